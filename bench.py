@@ -1,0 +1,217 @@
+#!/usr/bin/env python3
+"""bench.py — SHUD RHS flux assembly on MI355X: element-flux-updates/s (RHS evals x NumEle).
+
+Workload (BASELINE.json north_star / SURVEY §8d): synthetic 10M-triangle mesh (syn-10M: 3162 x 1582 quads,
+ccw-like river density, seed 12345), seeded random state y and ET-step inputs, serial (reference `make
+shud`) semantics.  One "step" = one RHS evaluation f(t, y, ydot) with y / ydot resident in HBM.
+N = 1: the whole mesh on one GPU.  N > 1 (torch.distributed.run, one process per GPU): the same 10M mesh
+partitioned by RCB across the N ranks, ghost states exchanged by RCCL (grouped send/recv over xGMI) inside
+every RHS call; value = NumEle_total x K / max-over-ranks time ("scaling": "strong", total work fixed).
+
+Prints ONE JSON line on rank 0 with roofline (dominant kernel: shud_ele_kernel, HIP-event timed on the
+stream it runs on) and cpu_baseline (the CPU restatement oracle on this host's cores, bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "shud-up_amd"))
+
+HBM_PEAK = 8.0e12          # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+METRIC = "element-flux-updates/sec (RHS evals × NumEle) at 1/2/4/8 GPUs; %HBM roofline"
+# algorithmic bytes per RHS (canonical): 392 B/element + 24 B/segment + 96 B/reach
+B_ELE, B_SEG, B_RIV = 392, 24, 96
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n-ele", type=int, default=10_000_000)
+    ap.add_argument("--mode", choices=["serial", "omp"], default="serial")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-reps", type=int, default=20)
+    ap.add_argument("--host-vectors", action="store_true", help="also time the PCIe-inclusive host-vector eval")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+
+    import torch
+    import torch.distributed as dist
+    from shud_rhs import abi, partition, runtime, synth, workload
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    mode = abi.SHUD_MODE_SERIAL if args.mode == "serial" else abi.SHUD_MODE_OMP
+
+    t0 = time.time()
+    gm = synth.synth_model(args.n_ele)
+    gm.step = workload.random_step_inputs(gm)
+    y_glob = workload.random_state(gm)
+    NE, NR, NS = gm.num_ele, gm.num_riv, gm.num_seg
+    log(f"[bench] syn mesh NE={NE} NR={NR} NS={NS} built in {time.time() - t0:.1f}s")
+
+    stream = torch.cuda.current_stream()
+    if world > 1:
+        _, _, plans = partition.build_plans(gm, world)
+        lm, part = partition.local_model(gm, plans[rank], rank, world)
+        uid = [runtime.nccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        part.nccl_unique_id = uid[0]
+        h = runtime.RhsHandle(lm, mode=mode, device=local, stream=stream.cuda_stream, partition=part)
+        y_loc = partition.local_state(y_glob, gm, part)
+        model = lm
+        log(f"[bench] rank0 partition: own {part.n_own_ele} ele / {part.n_own_riv} riv, "
+            f"ghosts {lm.num_ele - part.n_own_ele} ele / {lm.num_riv - part.n_own_riv} riv")
+    else:
+        h = runtime.RhsHandle(gm, mode=mode, device=local, stream=stream.cuda_stream)
+        y_loc = y_glob
+        model = gm
+    h.set_step_inputs()
+    y_t = torch.from_numpy(y_loc).to(f"cuda:{local}")
+    dy_t = torch.empty_like(y_t)
+    yp, dyp = y_t.data_ptr(), dy_t.data_ptr()
+
+    for _ in range(args.warmup):
+        h.eval_device(0.0, yp, dyp)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        h.eval_device(0.0, yp, dyp)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t_start
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    err = h.get_error()
+    if err["exit_code"]:
+        log(f"[bench] WARNING physics error flags {err}")
+
+    # per-kernel HIP-event timing on the handle's stream (= torch's current stream)
+    ms_eval, per = h.time_kernels(0.0, yp, dyp, args.profile_reps)
+    if world > 1:
+        dist.barrier()
+    ms_ele = per["shud_ele_kernel"]
+    ms_riv = per["shud_riv_kernel"]
+    n_own_e = model.num_ele if world == 1 else part.n_own_ele
+    n_own_r = model.num_riv if world == 1 else part.n_own_riv
+    n_seg_local = model.num_seg
+    ele_bytes = B_ELE * n_own_e + B_SEG * n_seg_local
+    riv_bytes = B_RIV * n_own_r
+    achieved = ele_bytes / (ms_ele * 1e-3)
+
+    value = NE * args.steps / dt
+    ms_step = dt / args.steps * 1e3
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "element-flux-updates/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "strong" if world > 1 else "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded jittered-grid Delaunay mesh + river tree, random y and ET-step inputs)",
+        "config": {"workload": f"syn-10M RHS ({args.mode} semantics)" if NE >= 9_000_000 else f"syn-{NE} RHS",
+                   "num_ele": NE, "num_riv": NR, "num_seg": NS,
+                   "parallelism": f"mesh-partition x{world} (RCB, RCCL halo)" if world > 1 else "single GPU",
+                   "y_ydot": "device-resident"},
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "shud_ele_kernel",
+            "achieved": achieved / 1e9,
+            "peak": HBM_PEAK / 1e9,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK,
+            "traffic": None,
+            "algorithmic_bytes_per_launch": ele_bytes,
+            "kernel_ms": {k: v for k, v in per.items()},
+            "rhs_frac": (ele_bytes + riv_bytes) / (ms_eval * 1e-3) / HBM_PEAK,
+        },
+        "cpu_baseline": None,
+    }
+    pmc = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    if os.path.exists(pmc) and world == 1:
+        try:
+            with open(pmc) as f:
+                pj = json.load(f)
+            if pj.get("num_ele") == NE and "shud_ele_kernel" in pj.get("kernels", {}):
+                out["roofline"]["traffic"] = pj["kernels"]["shud_ele_kernel"]["hbm_bytes_per_launch"]
+                out["roofline"]["traffic_source"] = "profiles/pmc_summary.json (rocprofv3 --pmc, corrected)"
+        except Exception as e:  # noqa: BLE001
+            log(f"[bench] could not read {pmc}: {e}")
+
+    if args.host_vectors and world == 1:
+        y_h = np.ascontiguousarray(y_loc)
+        dy_h = np.empty_like(y_h)
+        h.eval(0.0, y_h, dy_h)
+        th = time.perf_counter()
+        nrep = 5
+        for _ in range(nrep):
+            h.eval(0.0, y_h, dy_h, raise_on_physics=False)
+        out["host_vector_value"] = NE * nrep / (time.perf_counter() - th)
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(gm, y_glob, mode, args.cpu_seconds)
+    if world > 1:
+        dist.barrier()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    h.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(gm, y, mode, budget_s):
+    """The CPU restatement (oracle/, C + OpenMP, reference loop structure) on this host's cores, on the same
+    10M mesh and state: a bounded number of RHS calls (~budget_s of CPU work)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    threads = max(1, min(threads, len(os.sched_getaffinity(0))))
+    oracle.set_threads(threads)
+    o = oracle.OracleRhs(gm, mode)
+    o.set_step_inputs()
+    o.eval(0.0, y)                          # warm-up (first-touch)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        o.eval(0.0, y)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= 40:
+            break
+    return {"value": gm.num_ele * n / el, "unit": "element-flux-updates/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{n} RHS calls of the CPU restatement (oracle/shud_oracle.c, OpenMP {threads} threads) on "
+                      f"the full syn-10M mesh, {el:.1f}s wall"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,98 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes wrapper of oracle/liboracle.so (the CPU restatement in
+shud_oracle.c).  Used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the checker.
+Parity status: "parity unpinned" (see shud_oracle.c header and DESIGN.md §Oracle).
+"""
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "shud-up_amd"))
+from shud_rhs import abi  # noqa: E402  (struct layouts of include/shud_rhs.h)
+
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+_LIB = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        L.oracle_create.restype = C.c_void_p
+        L.oracle_create.argtypes = [C.POINTER(abi.ShudMeshSoA), C.POINTER(abi.ShudParamsSoA), C.c_int]
+        L.oracle_set_step_inputs.argtypes = [C.c_void_p, C.POINTER(abi.ShudStepInputs)]
+        L.oracle_f.restype = C.c_int
+        L.oracle_f.argtypes = [C.c_void_p, C.c_double, C.c_void_p, C.c_void_p]
+        L.oracle_get_diag.argtypes = [C.c_void_p, C.POINTER(abi.ShudFluxOut)]
+        L.oracle_destroy.argtypes = [C.c_void_p]
+        L.oracle_set_threads.argtypes = [C.c_int]
+        L.oracle_get_threads.restype = C.c_int
+        for n in ["oracle_exit_index", "oracle_exit_kind"]:
+            getattr(L, n).restype = C.c_int
+            getattr(L, n).argtypes = [C.c_void_p]
+        for n in ["oracle_num_calls", "oracle_num_warn"]:
+            getattr(L, n).restype = C.c_longlong
+            getattr(L, n).argtypes = [C.c_void_p]
+        _LIB = L
+    return _LIB
+
+
+def set_threads(n):
+    lib().oracle_set_threads(int(n))
+
+
+def get_threads():
+    return lib().oracle_get_threads()
+
+
+class OracleRhs:
+    """Same call sequence as shud_rhs.runtime.RhsHandle, evaluated by the CPU restatement."""
+
+    def __init__(self, model, mode=abi.SHUD_MODE_SERIAL):
+        self.model = model
+        self._mesh = model.mesh_struct()
+        self._par = model.params_struct()
+        self.h = lib().oracle_create(C.byref(self._mesh), C.byref(self._par), int(mode))
+        self.mode = mode
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().oracle_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def set_step_inputs(self, step=None, bc_tables=None):
+        s = self.model.step_struct(step, bc_tables)
+        lib().oracle_set_step_inputs(self.h, C.byref(s))
+
+    def eval(self, t, y):
+        """Returns (ydot, exit_code, exit_index, exit_kind)."""
+        y = np.ascontiguousarray(y, dtype=np.float64)
+        dy = np.zeros_like(y)
+        code = lib().oracle_f(self.h, float(t), y.ctypes.data, dy.ctypes.data)
+        return dy, code, lib().oracle_exit_index(self.h), lib().oracle_exit_kind(self.h)
+
+    def num_warn(self):
+        return lib().oracle_num_warn(self.h)
+
+    def diagnostics(self):
+        m = self.model
+        NE, NR, NS = m.num_ele, m.num_riv, m.num_seg
+        out, o = {}, abi.ShudFluxOut()
+        for name in abi.FLUXOUT_ORDER:
+            n = 3 * NE if name in abi.DIAG_ELE3 else NS if name in abi.DIAG_SEG else NR if name in abi.DIAG_RIV else NE
+            out[name] = np.zeros(n)
+            setattr(o, name, out[name].ctypes.data_as(abi.c_double_p))
+        lib().oracle_get_diag(self.h, C.byref(o))
+        return out

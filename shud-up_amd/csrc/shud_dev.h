@@ -1,0 +1,68 @@
+// shud_dev.h — device-side views shared by the kernels (shud_kernels.hip) and the host runtime
+// (shud_rhs.cpp).  All arrays are SoA in HBM; per-edge arrays are edge-major [3][num_ele].
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace shud {
+
+struct DevErr {                      // per-handle device error word (ShudErr on the host)
+    uint32_t flags;
+    int32_t first_index[8];          // slot = log2(bit); INT32_MAX = none
+    unsigned long long n_warn;
+};
+
+struct DevMesh {
+    int num_ele;                     // local elements incl. ghosts (per-edge stride)
+    // elements: topology + geometry
+    const int *nabr, *eflags;        // eflags: bits 0-15 iBC (int16), 16-17 iSS class (1: >0, 2: <0)
+    const double *area, *z_surf, *z_bottom, *depression, *edge, *dist2nabor, *dist2edge, *avg_rough, *rough;
+    // elements: hydraulic parameters
+    const double *aq, *macD, *macKsatH, *vAreaF, *KsatH, *KsatV, *infKsatV, *hAreaF, *macKsatV;
+    const double *ThetaS, *ThetaR, *Beta, *infD, *Sy, *RzD, *VegFrac, *ImpAF;
+    // per-ET-step inputs
+    const double *net_prep, *pot_evap, *pot_tran, *etp, *lai, *fu_surf, *fu_sub;
+    double *e_ic[2], *u_satn[2];     // carried state, ping-pong (read [cur], write [cur^1])
+    const double *ugw_stale;
+    const double *eybc, *eqbc, *rybc, *rqbc;
+    // segments in element-sorted order (stable in reference index)
+    const int *seg_off, *seg_riv;
+    const double *seg_len, *seg_cwr;
+    double *qseg_surf, *qseg_sub;
+    // reaches
+    const int *riv_down, *riv_bc;
+    const double *riv_len, *riv_slope, *riv_d2down, *riv_avg_rough, *riv_depth, *riv_bw, *riv_bankslope;
+    const double *riv_ksath, *riv_bedthick;
+    const int *up_off, *up_idx;      // upstream reaches of each owned reach, ascending
+    const int *rseg_off, *rseg_pos;  // segments of each owned reach, ascending reference order
+    DevErr *err;
+};
+
+struct DevDiag {                     // optional diagnostic outputs (ShudFluxOut), local numbering
+    double *qele_surf, *qele_sub, *qele_surf_tot, *qele_sub_tot, *q_infil, *q_exfil, *q_recharge;
+    double *q_es, *q_eu, *q_eg, *q_tu, *q_tg, *q_eta, *e_ic, *u_satn, *i_beta, *eff_kh;
+    double *qe2r_surf, *qe2r_sub, *qriv_down, *qriv_up, *qriv_surf, *qriv_sub;
+};
+
+// state accessors: owned entities read the caller's y, ghosts read the halo buffers
+struct YView {
+    const double *y;                 // owned block layout [sf|us|gw|riv] over owned counts
+    const double *gele;              // ghost elements, AoS records [3*k + {0,1,2}]
+    const double *griv;              // ghost reaches
+    int n_own, n_own_riv;
+#ifdef __HIPCC__
+    __device__ __forceinline__ double sf(int i) const { return i < n_own ? y[i] : gele[3 * (i - n_own)]; }
+    __device__ __forceinline__ double us(int i) const { return i < n_own ? y[n_own + i] : gele[3 * (i - n_own) + 1]; }
+    __device__ __forceinline__ double gw(int i) const { return i < n_own ? y[2 * n_own + i] : gele[3 * (i - n_own) + 2]; }
+    __device__ __forceinline__ double riv(int r) const { return r < n_own_riv ? y[3 * n_own + r] : griv[r - n_own_riv]; }
+#endif
+};
+
+void launch_element_kernel(const DevMesh &m, const YView &Y, double *dy, int n_compute, int cur, int cur_e,
+                           int mode, bool open, bool diag, const DevDiag &dg, hipStream_t s);
+void launch_river_kernel(const DevMesh &m, const YView &Y, double *dy, int mode, bool diag,
+                         const DevDiag &dg, hipStream_t s);
+void launch_pack_kernel(const double *y, int n_own, int n_own_riv, const int *eidx, int ne, const int *ridx,
+                        int nr, double *ebuf, double *rbuf, hipStream_t s);
+
+}  // namespace shud

@@ -1,0 +1,754 @@
+// shud_rhs.cpp — host runtime behind include/shud_rhs.h (C-ABI).
+//
+// Replaces the reference RHS callback f() (src/Model/f.cpp:2-32) and the Model_Data arrays it works
+// on (src/ModelData/Model_Data.hpp:111-208).  The handle owns device SoA copies of the static mesh and
+// parameters (uploaded once, shud_rhs_create), of the per-ET-step inputs (shud_rhs_set_step_inputs),
+// and of the carried RHS state (qEleE_IC, u_satn — ping-pong buffers so a diagnostic replay sees the
+// exact inputs of the last call).  y / ydot are borrowed per call.
+//
+// Multi-GPU: one process per GPU, each handle holds its partition (owned + ghost
+// entities); ghost states arrive by one grouped RCCL send/recv exchange (= ncclAllToAllv restricted
+// to the peers that share a boundary) per eval, before the element kernel.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "shud_dev.h"
+#include "shud_rhs.h"
+
+using namespace shud;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return fail(SHUD_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                        __FILE__, __LINE__);                                               \
+    } while (0)
+#define NCCL_TRY(expr)                                                                      \
+    do {                                                                                    \
+        ncclResult_t r_ = (expr);                                                           \
+        if (r_ != ncclSuccess)                                                              \
+            return fail(SHUD_ERR_NCCL, "%s failed: %s", #expr, ncclGetErrorString(r_));     \
+    } while (0)
+
+}  // namespace
+
+struct shud_rhs {
+    int NE = 0, NR = 0, NS = 0;          // local totals (incl. ghosts)
+    int n_own = 0, n_segghost = 0, n_own_riv = 0;
+    int mode = SHUD_MODE_SERIAL;
+    bool open = false;
+    bool check_errors = true;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    std::vector<void *> allocs;
+
+    DevMesh dm{};
+    DevDiag dd{};
+    bool have_diag = false;
+    int cur = 0, cur_e = 0;
+    long long ncalls = 0;
+
+    // host-pointer eval staging
+    double *d_y = nullptr, *d_ydot = nullptr, *d_scratch_dy = nullptr;
+    // replay info of the last eval
+    bool have_last = false;
+    const double *last_y = nullptr;
+    int last_cur = 0, last_cur_e = 0;
+
+    std::vector<int> seg_perm;           // element-sorted position -> reference segment index
+    int max_col[4] = {0, 0, 0, 0};       // highest BC column referenced: eyBC, eqBC, ryBC, rqBC
+    double *d_tab[4] = {nullptr, nullptr, nullptr, nullptr};
+    int tab_len[4] = {0, 0, 0, 0};
+
+    DevErr *d_err = nullptr;
+    DevErr *h_err = nullptr;             // pinned
+
+    // partition / halo
+    bool partitioned = false;
+    int rank = 0, nranks = 1;
+    bool use_nccl = false;
+    ncclComm_t comm = nullptr;
+    std::vector<int> esend_off, erecv_off, rsend_off, rrecv_off;
+    int *d_esend_idx = nullptr, *d_rsend_idx = nullptr;
+    int n_esend = 0, n_rsend = 0, n_eghost = 0, n_rghost = 0;
+    double *d_esend = nullptr, *d_rsend = nullptr, *d_gele = nullptr, *d_griv = nullptr;
+
+    template <class T>
+    int dalloc(T **p, size_t n) {
+        void *q = nullptr;
+        size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+        hipError_t e = hipMalloc(&q, bytes);
+        if (e != hipSuccess) return fail(SHUD_ERR_HIP, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+        allocs.push_back(q);
+        *p = (T *)q;
+        return 0;
+    }
+    template <class T>
+    int upload(T **p, const T *src, size_t n) {
+        int rc = dalloc(p, n);
+        if (rc) return rc;
+        if (n && src) HIP_TRY(hipMemcpy(*p, src, n * sizeof(T), hipMemcpyHostToDevice));
+        else if (n) HIP_TRY(hipMemset(*p, 0, n * sizeof(T)));
+        return 0;
+    }
+    template <class T>
+    int upload_fill(T **p, const T *src, size_t n, T fill) {
+        if (src) return upload(p, src, n);
+        std::vector<T> tmp(n, fill);
+        return upload(p, tmp.data(), n);
+    }
+};
+
+static int reset_err(shud_rhs *h) {
+    DevErr z{};
+    z.flags = 0;
+    for (int k = 0; k < 8; k++) z.first_index[k] = INT_MAX;
+    z.n_warn = 0;
+    HIP_TRY(hipMemcpyAsync(h->d_err, &z, sizeof(DevErr), hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+extern "C" int shud_rhs_abi_version(void) { return SHUD_RHS_ABI_VERSION; }
+extern "C" const char *shud_rhs_last_error_string(void) { return g_last_error.c_str(); }
+
+// ---------------------------------------------------------------------------------------------
+// create
+// ---------------------------------------------------------------------------------------------
+static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, const ShudRhsOptions *opt,
+                 const ShudPartition *part) {
+    const int NE = m->num_ele, NR = m->num_riv, NS = m->num_seg;
+    if (NE < 0 || NR < 0 || NS < 0) return fail(SHUD_ERR_ARG, "negative sizes");
+    h->NE = NE; h->NR = NR; h->NS = NS;
+    h->mode = opt ? opt->mode : SHUD_MODE_SERIAL;
+    if (h->mode != SHUD_MODE_SERIAL && h->mode != SHUD_MODE_OMP) return fail(SHUD_ERR_ARG, "bad mode %d", h->mode);
+    h->check_errors = opt ? opt->check_errors != 0 : true;
+    h->open = (m->close_boundary == 0);
+    h->device = opt ? opt->device : 0;
+    h->n_own = part ? part->n_own_ele : NE;
+    h->n_segghost = part ? part->n_segghost_ele : 0;
+    h->n_own_riv = part ? part->n_own_riv : NR;
+    if (h->n_own < 0 || h->n_own + h->n_segghost > NE || h->n_own_riv < 0 || h->n_own_riv > NR)
+        return fail(SHUD_ERR_ARG, "partition counts inconsistent with mesh sizes");
+
+    // ---- validation (the reference exits on these at run time; we reject them up front) ----
+    if (!m->nabr || !m->area || !m->z_surf || !m->z_bottom || !m->edge || !m->dist2nabor || !m->avg_rough)
+        return fail(SHUD_ERR_ARG, "missing element geometry array");
+    if (h->open && (!m->dist2edge || !m->rough)) return fail(SHUD_ERR_ARG, "open boundary needs dist2edge and rough");
+    if (NR && (!m->riv_down || !m->riv_length || !m->riv_bed_slope || !m->riv_dist2down || !m->riv_avg_rough ||
+               !m->riv_depth || !m->riv_bottom_width || !m->riv_bankslope || !m->riv_ksath || !m->riv_bedthick))
+        return fail(SHUD_ERR_ARG, "missing river array");
+    if (NS && (!m->seg_ele || !m->seg_riv || !m->seg_length || !m->seg_cwr)) return fail(SHUD_ERR_ARG, "missing segment array");
+    const double *pp[17] = {p->aquifer_depth, p->macD, p->macKsatH, p->geo_vAreaF, p->KsatH, p->KsatV,
+                            p->infKsatV, p->hAreaF, p->macKsatV, p->ThetaS, p->ThetaR, p->Beta,
+                            p->infD, p->Sy, p->RzD, p->VegFrac, p->ImpAF};
+    for (int k = 0; k < 17; k++)
+        if (!pp[k]) return fail(SHUD_ERR_ARG, "missing parameter array #%d", k);
+    for (long long q = 0; q < 3LL * NE; q++)
+        if (m->nabr[q] < -1 || m->nabr[q] >= NE) return fail(SHUD_ERR_ARG, "nabr[%lld]=%d out of range", q, m->nabr[q]);
+    if (m->ilake)
+        for (int i = 0; i < NE; i++)
+            if (m->ilake[i] > 0) return fail(SHUD_ERR_UNSUPPORTED, "lake element %d: lake module not supported", i);
+    for (int r = 0; r < NR; r++) {
+        int d = m->riv_down[r];
+        if (d >= NR || (d < 0 && d < -4))
+            return fail(SHUD_ERR_ARG, "Fatal Error: River Routing Boundary Condition Type Is Wrong! (reach %d down %d)", r, d);
+    }
+    for (int s = 0; s < NS; s++)
+        if (m->seg_ele[s] < 0 || m->seg_ele[s] >= NE || m->seg_riv[s] < 0 || m->seg_riv[s] >= NR)
+            return fail(SHUD_ERR_ARG, "segment %d references element/reach out of range", s);
+
+    // ---- packed element flags, BC column maxima ----
+    std::vector<int> eflags(NE);
+    for (int i = 0; i < NE; i++) {
+        int ibc = m->ibc ? m->ibc[i] : 0, iss = m->iss ? m->iss[i] : 0;
+        if (ibc < -32768 || ibc > 32767) return fail(SHUD_ERR_ARG, "iBC out of range at %d", i);
+        eflags[i] = (ibc & 0xffff) | ((iss > 0 ? 1 : iss < 0 ? 2 : 0) << 16);
+        if (ibc > 0) h->max_col[0] = std::max(h->max_col[0], ibc);
+        if (ibc < 0) h->max_col[1] = std::max(h->max_col[1], -ibc);
+    }
+    std::vector<int> rbc(NR, 0);
+    for (int r = 0; r < NR; r++) {
+        rbc[r] = m->riv_bc ? m->riv_bc[r] : 0;
+        if (rbc[r] > 0) h->max_col[2] = std::max(h->max_col[2], rbc[r]);
+        if (rbc[r] < 0) h->max_col[3] = std::max(h->max_col[3], -rbc[r]);
+    }
+
+    // ---- segment CSR by element (stable: ascending reference index inside an element) ----
+    const int ncomp = h->n_own + h->n_segghost;
+    std::vector<int> order(NS);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return m->seg_ele[a] < m->seg_ele[b]; });
+    std::vector<int> seg_off(NE + 1, 0), seg_riv(NS), pos_of(NS);
+    std::vector<double> seg_len(NS), seg_cwr(NS);
+    for (int s = 0; s < NS; s++) seg_off[m->seg_ele[s] + 1]++;
+    for (int i = 0; i < NE; i++) seg_off[i + 1] += seg_off[i];
+    for (int k = 0; k < NS; k++) {
+        int s = order[k];
+        seg_riv[k] = m->seg_riv[s];
+        seg_len[k] = m->seg_length[s];
+        seg_cwr[k] = m->seg_cwr[s];
+        pos_of[s] = k;
+    }
+    // only elements < ncomp compute their segments; segments of pure ghosts must not be needed
+    for (int s = 0; s < NS; s++)
+        if (m->seg_ele[s] >= ncomp && m->seg_riv[s] < h->n_own_riv)
+            return fail(SHUD_ERR_ARG, "segment %d of an owned reach belongs to a non-computed ghost element", s);
+    h->seg_perm = order;
+    // ---- per owned reach: its segments (ascending reference order) and upstream reaches ----
+    std::vector<int> rseg_off(h->n_own_riv + 1, 0), rseg_pos;
+    for (int s = 0; s < NS; s++)
+        if (m->seg_riv[s] < h->n_own_riv) rseg_off[m->seg_riv[s] + 1]++;
+    for (int r = 0; r < h->n_own_riv; r++) rseg_off[r + 1] += rseg_off[r];
+    rseg_pos.resize(rseg_off[h->n_own_riv]);
+    {
+        std::vector<int> fillp(rseg_off.begin(), rseg_off.end() - 1);
+        for (int s = 0; s < NS; s++) {
+            int r = m->seg_riv[s];
+            if (r < h->n_own_riv) rseg_pos[fillp[r]++] = pos_of[s];
+        }
+    }
+    std::vector<int> up_off(h->n_own_riv + 1, 0), up_idx;
+    for (int r = 0; r < NR; r++) {
+        int d = m->riv_down[r];
+        if (d >= 0 && d < h->n_own_riv) up_off[d + 1]++;
+    }
+    for (int r = 0; r < h->n_own_riv; r++) up_off[r + 1] += up_off[r];
+    up_idx.resize(up_off[h->n_own_riv]);
+    {
+        // ascending reach order (MD_f.cpp:236-240); in a partition, ascending GLOBAL reach id
+        std::vector<int> fillp(up_off.begin(), up_off.end() - 1);
+        for (int r = 0; r < NR; r++) {
+            int d = m->riv_down[r];
+            if (d >= 0 && d < h->n_own_riv) up_idx[fillp[d]++] = r;
+        }
+        if (part && part->riv_gid)
+            for (int r = 0; r < h->n_own_riv; r++)
+                std::sort(up_idx.begin() + up_off[r], up_idx.begin() + up_off[r + 1],
+                          [&](int a, int b) { return part->riv_gid[a] < part->riv_gid[b]; });
+    }
+
+    // ---- device ----
+    HIP_TRY(hipSetDevice(h->device));
+    if (opt && opt->stream) {
+        h->stream = (hipStream_t)opt->stream;
+    } else {
+        HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+        h->own_stream = true;
+    }
+    DevMesh &d = h->dm;
+    d.num_ele = NE;
+    int rc = 0;
+#define UP(field, src, n) if ((rc = h->upload(&field##_w, src, n))) return rc; d.field = field##_w
+    {
+        int *nabr_w, *eflags_w;
+        double *area_w, *z_surf_w, *z_bottom_w, *depression_w, *edge_w, *dist2nabor_w, *dist2edge_w, *avg_rough_w, *rough_w;
+        UP(nabr, m->nabr, 3 * (size_t)NE);
+        UP(eflags, eflags.data(), NE);
+        UP(area, m->area, NE);
+        UP(z_surf, m->z_surf, NE);
+        UP(z_bottom, m->z_bottom, NE);
+        if ((rc = h->upload_fill(&depression_w, m->depression, NE, 0.0002))) return rc;
+        d.depression = depression_w;
+        UP(edge, m->edge, 3 * (size_t)NE);
+        UP(dist2nabor, m->dist2nabor, 3 * (size_t)NE);
+        UP(avg_rough, m->avg_rough, 3 * (size_t)NE);
+        UP(dist2edge, h->open ? m->dist2edge : (const double *)nullptr, h->open ? 3 * (size_t)NE : 1);
+        UP(rough, h->open ? m->rough : (const double *)nullptr, h->open ? (size_t)NE : 1);
+    }
+    {
+        double *aq_w, *macD_w, *macKsatH_w, *vAreaF_w, *KsatH_w, *KsatV_w, *infKsatV_w, *hAreaF_w, *macKsatV_w;
+        double *ThetaS_w, *ThetaR_w, *Beta_w, *infD_w, *Sy_w, *RzD_w, *VegFrac_w, *ImpAF_w;
+        UP(aq, p->aquifer_depth, NE); UP(macD, p->macD, NE); UP(macKsatH, p->macKsatH, NE);
+        UP(vAreaF, p->geo_vAreaF, NE); UP(KsatH, p->KsatH, NE); UP(KsatV, p->KsatV, NE);
+        UP(infKsatV, p->infKsatV, NE); UP(hAreaF, p->hAreaF, NE); UP(macKsatV, p->macKsatV, NE);
+        UP(ThetaS, p->ThetaS, NE); UP(ThetaR, p->ThetaR, NE); UP(Beta, p->Beta, NE); UP(infD, p->infD, NE);
+        UP(Sy, p->Sy, NE); UP(RzD, p->RzD, NE); UP(VegFrac, p->VegFrac, NE); UP(ImpAF, p->ImpAF, NE);
+    }
+    {
+        double *net_prep_w, *pot_evap_w, *pot_tran_w, *etp_w, *lai_w, *fu_surf_w, *fu_sub_w, *ugw_stale_w;
+        UP(net_prep, (const double *)nullptr, NE); UP(pot_evap, (const double *)nullptr, NE); UP(pot_tran, (const double *)nullptr, NE); UP(etp, (const double *)nullptr, NE);
+        UP(lai, (const double *)nullptr, NE);
+        if ((rc = h->upload_fill(&fu_surf_w, (const double *)nullptr, NE, 1.0))) return rc;
+        d.fu_surf = fu_surf_w;
+        if ((rc = h->upload_fill(&fu_sub_w, (const double *)nullptr, NE, 1.0))) return rc;
+        d.fu_sub = fu_sub_w;
+        UP(ugw_stale, (const double *)nullptr, NE);
+        for (int k = 0; k < 2; k++) {
+            if ((rc = h->upload(&d.e_ic[k], (const double *)nullptr, NE))) return rc;
+            if ((rc = h->upload(&d.u_satn[k], (const double *)nullptr, NE))) return rc;
+        }
+    }
+    for (int k = 0; k < 4; k++) {
+        h->tab_len[k] = h->max_col[k] + 1;
+        if ((rc = h->upload(&h->d_tab[k], (const double *)nullptr, h->tab_len[k]))) return rc;
+    }
+    d.eybc = h->d_tab[0]; d.eqbc = h->d_tab[1]; d.rybc = h->d_tab[2]; d.rqbc = h->d_tab[3];
+    {
+        int *seg_off_w, *seg_riv_w;
+        double *seg_len_w, *seg_cwr_w;
+        UP(seg_off, seg_off.data(), NE + 1);
+        UP(seg_riv, seg_riv.data(), NS);
+        UP(seg_len, seg_len.data(), NS);
+        UP(seg_cwr, seg_cwr.data(), NS);
+        if ((rc = h->upload(&d.qseg_surf, (const double *)nullptr, NS))) return rc;
+        if ((rc = h->upload(&d.qseg_sub, (const double *)nullptr, NS))) return rc;
+    }
+    {
+        int *riv_down_w, *riv_bc_w, *up_off_w, *up_idx_w, *rseg_off_w, *rseg_pos_w;
+        double *riv_len_w, *riv_slope_w, *riv_d2down_w, *riv_avg_rough_w, *riv_depth_w, *riv_bw_w,
+            *riv_bankslope_w, *riv_ksath_w, *riv_bedthick_w;
+        UP(riv_down, m->riv_down, NR); UP(riv_bc, rbc.data(), NR);
+        UP(riv_len, m->riv_length, NR); UP(riv_slope, m->riv_bed_slope, NR); UP(riv_d2down, m->riv_dist2down, NR);
+        UP(riv_avg_rough, m->riv_avg_rough, NR); UP(riv_depth, m->riv_depth, NR); UP(riv_bw, m->riv_bottom_width, NR);
+        UP(riv_bankslope, m->riv_bankslope, NR); UP(riv_ksath, m->riv_ksath, NR); UP(riv_bedthick, m->riv_bedthick, NR);
+        UP(up_off, up_off.data(), up_off.size()); UP(up_idx, up_idx.data(), up_idx.size());
+        UP(rseg_off, rseg_off.data(), rseg_off.size()); UP(rseg_pos, rseg_pos.data(), rseg_pos.size());
+    }
+#undef UP
+    if ((rc = h->dalloc(&h->d_err, 1))) return rc;
+    d.err = h->d_err;
+    HIP_TRY(hipHostMalloc((void **)&h->h_err, sizeof(DevErr), hipHostMallocDefault));
+    if ((rc = reset_err(h))) return rc;
+    const size_t ny = 3 * (size_t)h->n_own + h->n_own_riv;
+    if ((rc = h->dalloc(&h->d_y, ny))) return rc;
+    if ((rc = h->dalloc(&h->d_ydot, ny))) return rc;
+    if ((rc = h->dalloc(&h->d_scratch_dy, ny))) return rc;
+    return 0;
+}
+
+static int setup_partition(shud_rhs *h, const ShudPartition *part) {
+    h->partitioned = true;
+    h->rank = part->rank;
+    h->nranks = part->nranks;
+    const int P = part->nranks;
+    if (P < 1 || part->rank < 0 || part->rank >= P) return fail(SHUD_ERR_ARG, "bad rank/nranks");
+    h->esend_off.assign(part->ele_send_off, part->ele_send_off + P + 1);
+    h->erecv_off.assign(part->ele_recv_off, part->ele_recv_off + P + 1);
+    h->rsend_off.assign(part->riv_send_off, part->riv_send_off + P + 1);
+    h->rrecv_off.assign(part->riv_recv_off, part->riv_recv_off + P + 1);
+    h->n_esend = h->esend_off[P];
+    h->n_rsend = h->rsend_off[P];
+    h->n_eghost = h->erecv_off[P];
+    h->n_rghost = h->rrecv_off[P];
+    if (h->n_own + h->n_eghost != h->NE) return fail(SHUD_ERR_ARG, "ghost element count mismatch");
+    if (h->n_own_riv + h->n_rghost != h->NR) return fail(SHUD_ERR_ARG, "ghost reach count mismatch");
+    for (int k = 0; k < h->n_esend; k++)
+        if (part->ele_send_idx[k] < 0 || part->ele_send_idx[k] >= h->n_own) return fail(SHUD_ERR_ARG, "bad ele_send_idx");
+    for (int k = 0; k < h->n_rsend; k++)
+        if (part->riv_send_idx[k] < 0 || part->riv_send_idx[k] >= h->n_own_riv) return fail(SHUD_ERR_ARG, "bad riv_send_idx");
+    int rc;
+    if ((rc = h->upload(&h->d_esend_idx, part->ele_send_idx, h->n_esend))) return rc;
+    if ((rc = h->upload(&h->d_rsend_idx, part->riv_send_idx, h->n_rsend))) return rc;
+    if ((rc = h->dalloc(&h->d_esend, 3 * (size_t)h->n_esend))) return rc;
+    if ((rc = h->dalloc(&h->d_rsend, (size_t)h->n_rsend))) return rc;
+    if ((rc = h->dalloc(&h->d_gele, 3 * (size_t)h->n_eghost))) return rc;
+    if ((rc = h->dalloc(&h->d_griv, (size_t)h->n_rghost))) return rc;
+    if (part->nccl_unique_id) {
+        ncclUniqueId id;
+        memcpy(&id, part->nccl_unique_id, sizeof(id));
+        h->use_nccl = true;
+        NCCL_TRY(ncclCommInitRank(&h->comm, P, id, part->rank));
+    }
+    return 0;
+}
+
+static void destroy_handle(shud_rhs *h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->comm) ncclCommDestroy(h->comm);
+    for (void *p : h->allocs) (void)hipFree(p);
+    if (h->h_err) (void)hipHostFree(h->h_err);
+    if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+extern "C" int shud_rhs_create(const ShudMeshSoA *mesh, const ShudParamsSoA *par, const ShudRhsOptions *opt,
+                               shud_rhs_t *out) {
+    if (!mesh || !par || !out) return fail(SHUD_ERR_ARG, "null argument");
+    shud_rhs *h = new shud_rhs();
+    int rc = build(h, mesh, par, opt, nullptr);
+    if (rc) { destroy_handle(h); return rc; }
+    *out = h;
+    return SHUD_OK;
+}
+
+extern "C" int shud_rhs_nccl_unique_id(char out[128]) {
+    ncclUniqueId id;
+    NCCL_TRY(ncclGetUniqueId(&id));
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    memcpy(out, &id, sizeof(id));
+    return SHUD_OK;
+}
+
+extern "C" int shud_rhs_create_partitioned(const ShudMeshSoA *mesh, const ShudParamsSoA *par,
+                                           const ShudRhsOptions *opt, const ShudPartition *part,
+                                           shud_rhs_t *out) {
+    if (!mesh || !par || !part || !out) return fail(SHUD_ERR_ARG, "null argument");
+    shud_rhs *h = new shud_rhs();
+    int rc = build(h, mesh, par, opt, part);
+    if (!rc) rc = setup_partition(h, part);
+    if (rc) { destroy_handle(h); return rc; }
+    *out = h;
+    return SHUD_OK;
+}
+
+extern "C" int shud_rhs_destroy(shud_rhs_t h) {
+    destroy_handle(h);
+    return SHUD_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// step inputs
+// ---------------------------------------------------------------------------------------------
+extern "C" int shud_rhs_set_step_inputs(shud_rhs_t h, const ShudStepInputs *in) {
+    if (!h || !in) return fail(SHUD_ERR_ARG, "null argument");
+    HIP_TRY(hipSetDevice(h->device));
+    const size_t nb = (size_t)h->NE * sizeof(double);
+    struct { const double *src; const double *dst; } arr[] = {
+        {in->net_prep, h->dm.net_prep}, {in->pot_evap, h->dm.pot_evap}, {in->pot_tran, h->dm.pot_tran},
+        {in->etp, h->dm.etp}, {in->lai, h->dm.lai}, {in->fu_surf, h->dm.fu_surf}, {in->fu_sub, h->dm.fu_sub},
+        {in->ugw_stale, h->dm.ugw_stale}, {in->e_ic, h->dm.e_ic[h->cur_e]}, {in->u_satn, h->dm.u_satn[h->cur]}};
+    for (auto &a : arr)
+        if (a.src) HIP_TRY(hipMemcpyAsync((void *)a.dst, a.src, nb, hipMemcpyHostToDevice, h->stream));
+    const double *tabs[4] = {in->ele_ybc, in->ele_qbc, in->riv_ybc, in->riv_qbc};
+    const int ns[4] = {in->n_ele_ybc, in->n_ele_qbc, in->n_riv_ybc, in->n_riv_qbc};
+    for (int k = 0; k < 4; k++) {
+        if (!tabs[k]) continue;
+        if (ns[k] < h->max_col[k])
+            return fail(SHUD_ERR_ARG, "BC table %d has %d columns, mesh references column %d", k, ns[k], h->max_col[k]);
+        HIP_TRY(hipMemcpyAsync(h->d_tab[k], tabs[k], (size_t)h->tab_len[k] * sizeof(double), hipMemcpyHostToDevice,
+                               h->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    h->have_last = false;
+    return SHUD_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// eval
+// ---------------------------------------------------------------------------------------------
+static int exchange(shud_rhs *h, const double *y) {
+    if (!h->partitioned) return 0;
+    launch_pack_kernel(y, h->n_own, h->n_own_riv, h->d_esend_idx, h->n_esend, h->d_rsend_idx, h->n_rsend,
+                       h->d_esend, h->d_rsend, h->stream);
+    if (!h->use_nccl) return 0;      // external transport (tests): caller moved the buffers
+    NCCL_TRY(ncclGroupStart());
+    for (int p = 0; p < h->nranks; p++) {
+        if (p == h->rank) continue;
+        size_t se = h->esend_off[p + 1] - h->esend_off[p], re = h->erecv_off[p + 1] - h->erecv_off[p];
+        size_t sr = h->rsend_off[p + 1] - h->rsend_off[p], rr = h->rrecv_off[p + 1] - h->rrecv_off[p];
+        if (se) NCCL_TRY(ncclSend(h->d_esend + 3 * (size_t)h->esend_off[p], 3 * se, ncclDouble, p, h->comm, h->stream));
+        if (re) NCCL_TRY(ncclRecv(h->d_gele + 3 * (size_t)h->erecv_off[p], 3 * re, ncclDouble, p, h->comm, h->stream));
+        if (sr) NCCL_TRY(ncclSend(h->d_rsend + h->rsend_off[p], sr, ncclDouble, p, h->comm, h->stream));
+        if (rr) NCCL_TRY(ncclRecv(h->d_griv + h->rrecv_off[p], rr, ncclDouble, p, h->comm, h->stream));
+    }
+    NCCL_TRY(ncclGroupEnd());
+    return 0;
+}
+
+static void launch_all(shud_rhs *h, const double *y, double *dy, int cur, int cur_e, bool diag) {
+    YView Y{y, h->d_gele, h->d_griv, h->n_own, h->n_own_riv};
+    launch_element_kernel(h->dm, Y, dy, h->n_own + h->n_segghost, cur, cur_e, h->mode, h->open, diag, h->dd,
+                          h->stream);
+    launch_river_kernel(h->dm, Y, dy, h->mode, diag, h->dd, h->stream);
+}
+
+static int read_err(shud_rhs *h) {
+    HIP_TRY(hipMemcpyAsync(h->h_err, h->d_err, sizeof(DevErr), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+static const uint32_t kFatal = SHUD_EF_NAN_QELE | SHUD_EF_EFFKH | SHUD_EF_ET_NEG | SHUD_EF_ET_NAN;
+
+static int eval_device(shud_rhs *h, double t, const double *y, double *dy) {
+    (void)t;
+    int rc = exchange(h, y);
+    if (rc) return rc;
+    h->last_cur = h->cur;
+    h->last_cur_e = h->cur_e;
+    launch_all(h, y, dy, h->cur, h->cur_e, false);
+    HIP_TRY(hipGetLastError());
+    h->cur ^= 1;
+    if (h->mode == SHUD_MODE_SERIAL) h->cur_e ^= 1;
+    h->last_y = y;
+    h->have_last = true;
+    h->ncalls++;
+    return 0;
+}
+
+extern "C" int shud_rhs_eval(shud_rhs_t h, double t, const double *y, double *ydot, int where) {
+    if (!h || !y || !ydot) return fail(SHUD_ERR_ARG, "null argument");
+    const size_t ny = 3 * (size_t)h->n_own + h->n_own_riv;
+    if (where == SHUD_WHERE_DEVICE) return eval_device(h, t, y, ydot);
+    if (where != SHUD_WHERE_HOST) return fail(SHUD_ERR_ARG, "bad where");
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipMemcpyAsync(h->d_y, y, ny * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    int rc = eval_device(h, t, h->d_y, h->d_ydot);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(ydot, h->d_ydot, ny * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    if (h->check_errors) {
+        if ((rc = read_err(h))) return rc;
+        if (h->h_err->flags & kFatal) return fail(SHUD_ERR_PHYSICS, "physics error flags 0x%x", h->h_err->flags);
+    } else {
+        HIP_TRY(hipStreamSynchronize(h->stream));
+    }
+    return SHUD_OK;
+}
+
+extern "C" long long shud_rhs_num_calls(shud_rhs_t h) { return h ? h->ncalls : -1; }
+
+// ---------------------------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------------------------
+extern "C" int shud_rhs_get_error(shud_rhs_t h, ShudErr *e) {
+    if (!h || !e) return fail(SHUD_ERR_ARG, "null argument");
+    HIP_TRY(hipSetDevice(h->device));
+    int rc = read_err(h);
+    if (rc) return rc;
+    const DevErr &d = *h->h_err;
+    memset(e, 0, sizeof(*e));
+    e->flags = d.flags;
+    for (int k = 0; k < 8; k++) e->first_index[k] = (d.first_index[k] == INT_MAX) ? -1 : d.first_index[k];
+    e->n_aet_warn = (int64_t)d.n_warn;
+    // the reference stops at the first myexit() in loop order: loop A (f_etFlux then effKH, per element,
+    // MD_f.cpp:11-26), then the applyDY NaN check (MD_f.cpp:73-74)
+    int et = INT_MAX;
+    if (d.flags & SHUD_EF_ET_NEG) et = std::min(et, d.first_index[2]);
+    if (d.flags & SHUD_EF_ET_NAN) et = std::min(et, d.first_index[3]);
+    int kh = (d.flags & SHUD_EF_EFFKH) ? d.first_index[1] : INT_MAX;
+    if (et != INT_MAX || kh != INT_MAX) {
+        if (et <= kh) {
+            e->exit_code = 10;
+            bool neg = (d.flags & SHUD_EF_ET_NEG) && d.first_index[2] == et;
+            snprintf(e->message, sizeof(e->message), neg ? "ERROR: Negative ET flux of Element %d is not allowed."
+                                                         : "ERROR: NAN error for ET flux %d", et + 1);
+        } else {
+            e->exit_code = 13;
+            snprintf(e->message, sizeof(e->message), "Wrong effKH for ground water (element %d)", kh + 1);
+        }
+    } else if (d.flags & SHUD_EF_NAN_QELE) {
+        e->exit_code = 10;
+        snprintf(e->message, sizeof(e->message), "ERROR: NAN error for QeleSurf/QeleSub %d", d.first_index[0] + 1);
+    }
+    return SHUD_OK;
+}
+
+extern "C" int shud_rhs_clear_error(shud_rhs_t h) {
+    if (!h) return fail(SHUD_ERR_ARG, "null argument");
+    return reset_err(h);
+}
+
+extern "C" int shud_rhs_cvrhs(double t, const double *y, double *ydot, void *user_data) {
+    shud_rhs *h = (shud_rhs *)user_data;
+    int rc = shud_rhs_eval(h, t, y, ydot, SHUD_WHERE_HOST);
+    if (rc == SHUD_OK) return 0;
+    const char *strict = getenv("SHUD_RHS_STRICT_EXIT");
+    if (rc == SHUD_ERR_PHYSICS && strict && strict[0] == '1') {
+        ShudErr e;
+        shud_rhs_get_error(h, &e);
+        printf("\n%s\n", e.message);
+        fprintf(stderr, "\nEXIT with error code %d\n", e.exit_code);
+        exit(e.exit_code);
+    }
+    return -1;
+}
+
+// ---------------------------------------------------------------------------------------------
+// diagnostics (replay of the last call with DIAG kernels)
+// ---------------------------------------------------------------------------------------------
+static int ensure_diag(shud_rhs *h) {
+    if (h->have_diag) return 0;
+    const size_t NE = h->NE, NR = h->NR;
+    double **e1[] = {&h->dd.qele_surf_tot, &h->dd.qele_sub_tot, &h->dd.q_infil, &h->dd.q_exfil, &h->dd.q_recharge,
+                     &h->dd.q_es, &h->dd.q_eu, &h->dd.q_eg, &h->dd.q_tu, &h->dd.q_tg, &h->dd.q_eta,
+                     &h->dd.e_ic, &h->dd.u_satn, &h->dd.i_beta, &h->dd.eff_kh, &h->dd.qe2r_surf, &h->dd.qe2r_sub};
+    int rc;
+    for (auto pp : e1)
+        if ((rc = h->upload(pp, (const double *)nullptr, NE))) return rc;
+    if ((rc = h->upload(&h->dd.qele_surf, (const double *)nullptr, 3 * NE))) return rc;
+    if ((rc = h->upload(&h->dd.qele_sub, (const double *)nullptr, 3 * NE))) return rc;
+    double **r1[] = {&h->dd.qriv_down, &h->dd.qriv_up, &h->dd.qriv_surf, &h->dd.qriv_sub};
+    for (auto pp : r1)
+        if ((rc = h->upload(pp, (const double *)nullptr, NR))) return rc;
+    h->have_diag = true;
+    return 0;
+}
+
+extern "C" int shud_rhs_sync_diagnostics(shud_rhs_t h, ShudFluxOut *o) {
+    if (!h || !o) return fail(SHUD_ERR_ARG, "null argument");
+    if (!h->have_last) return fail(SHUD_ERR_ARG, "no evaluation to report diagnostics for");
+    HIP_TRY(hipSetDevice(h->device));
+    int rc = ensure_diag(h);
+    if (rc) return rc;
+    // replay: same y, same carried-state inputs; it rewrites the same carried outputs
+    launch_all(h, h->last_y, h->d_scratch_dy, h->last_cur, h->last_cur_e, true);
+    HIP_TRY(hipGetLastError());
+    const size_t NE = h->NE, NR = h->NR, NS = h->NS;
+    auto get = [&](double *dst, const double *src, size_t n) -> int {
+        if (dst && n) HIP_TRY(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+        return 0;
+    };
+    const DevDiag &g = h->dd;
+    if ((rc = get(o->qele_surf, g.qele_surf, 3 * NE)) || (rc = get(o->qele_sub, g.qele_sub, 3 * NE)) ||
+        (rc = get(o->qele_surf_tot, g.qele_surf_tot, NE)) || (rc = get(o->qele_sub_tot, g.qele_sub_tot, NE)) ||
+        (rc = get(o->q_infil, g.q_infil, NE)) || (rc = get(o->q_exfil, g.q_exfil, NE)) ||
+        (rc = get(o->q_recharge, g.q_recharge, NE)) || (rc = get(o->q_es, g.q_es, NE)) ||
+        (rc = get(o->q_eu, g.q_eu, NE)) || (rc = get(o->q_eg, g.q_eg, NE)) || (rc = get(o->q_tu, g.q_tu, NE)) ||
+        (rc = get(o->q_tg, g.q_tg, NE)) || (rc = get(o->q_eta, g.q_eta, NE)) || (rc = get(o->e_ic, g.e_ic, NE)) ||
+        (rc = get(o->u_satn, g.u_satn, NE)) || (rc = get(o->i_beta, g.i_beta, NE)) ||
+        (rc = get(o->eff_kh, g.eff_kh, NE)) || (rc = get(o->qe2r_surf, g.qe2r_surf, NE)) ||
+        (rc = get(o->qe2r_sub, g.qe2r_sub, NE)) || (rc = get(o->qriv_down, g.qriv_down, NR)) ||
+        (rc = get(o->qriv_up, g.qriv_up, NR)) || (rc = get(o->qriv_surf, g.qriv_surf, NR)) ||
+        (rc = get(o->qriv_sub, g.qriv_sub, NR)))
+        return rc;
+    std::vector<double> tmp;
+    if (o->qseg_surf || o->qseg_sub) tmp.resize(std::max<size_t>(NS, 1));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    if (o->qseg_surf) {
+        HIP_TRY(hipMemcpy(tmp.data(), h->dm.qseg_surf, NS * sizeof(double), hipMemcpyDeviceToHost));
+        for (size_t k = 0; k < NS; k++) o->qseg_surf[h->seg_perm[k]] = tmp[k];
+    }
+    if (o->qseg_sub) {
+        HIP_TRY(hipMemcpy(tmp.data(), h->dm.qseg_sub, NS * sizeof(double), hipMemcpyDeviceToHost));
+        for (size_t k = 0; k < NS; k++) o->qseg_sub[h->seg_perm[k]] = tmp[k];
+    }
+    return SHUD_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// measurement helpers
+// ---------------------------------------------------------------------------------------------
+extern "C" int shud_rhs_device_alloc(shud_rhs_t h, size_t bytes, void **dptr) {
+    if (!h || !dptr) return fail(SHUD_ERR_ARG, "null argument");
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipMalloc(dptr, bytes ? bytes : 8));
+    return SHUD_OK;
+}
+extern "C" int shud_rhs_device_free(shud_rhs_t h, void *dptr) {
+    (void)h;
+    HIP_TRY(hipFree(dptr));
+    return SHUD_OK;
+}
+extern "C" int shud_rhs_memcpy(shud_rhs_t h, void *dst, const void *src, size_t bytes, int kind) {
+    if (!h) return fail(SHUD_ERR_ARG, "null argument");
+    hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : kind == 2 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, k, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return SHUD_OK;
+}
+extern "C" int shud_rhs_synchronize(shud_rhs_t h) {
+    if (!h) return fail(SHUD_ERR_ARG, "null argument");
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return SHUD_OK;
+}
+extern "C" void *shud_rhs_stream(shud_rhs_t h) { return h ? (void *)h->stream : nullptr; }
+
+// halo buffers of a partitioned handle (external-transport tests move them between handles)
+extern "C" int shud_rhs_halo_buffers(shud_rhs_t h, double **esend, double **rsend, double **gele, double **griv) {
+    if (!h || !h->partitioned) return fail(SHUD_ERR_ARG, "not a partitioned handle");
+    *esend = h->d_esend; *rsend = h->d_rsend; *gele = h->d_gele; *griv = h->d_griv;
+    return SHUD_OK;
+}
+// split eval for external transport: pack, (caller exchanges), compute
+extern "C" int shud_rhs_eval_pack(shud_rhs_t h, const double *d_y) {
+    if (!h || !h->partitioned) return fail(SHUD_ERR_ARG, "not a partitioned handle");
+    launch_pack_kernel(d_y, h->n_own, h->n_own_riv, h->d_esend_idx, h->n_esend, h->d_rsend_idx, h->n_rsend,
+                       h->d_esend, h->d_rsend, h->stream);
+    HIP_TRY(hipGetLastError());
+    return SHUD_OK;
+}
+extern "C" int shud_rhs_eval_compute(shud_rhs_t h, double t, const double *d_y, double *d_ydot) {
+    (void)t;
+    if (!h) return fail(SHUD_ERR_ARG, "null argument");
+    h->last_cur = h->cur;
+    h->last_cur_e = h->cur_e;
+    launch_all(h, d_y, d_ydot, h->cur, h->cur_e, false);
+    HIP_TRY(hipGetLastError());
+    h->cur ^= 1;
+    if (h->mode == SHUD_MODE_SERIAL) h->cur_e ^= 1;
+    h->last_y = d_y;
+    h->have_last = true;
+    h->ncalls++;
+    return SHUD_OK;
+}
+
+extern "C" int shud_rhs_time_kernels(shud_rhs_t h, double t, const double *d_y, double *d_ydot, int reps,
+                                     double *ms_eval, double *ms_out, int *nk, char *names_out, int names_len) {
+    (void)t;
+    if (!h || reps <= 0) return fail(SHUD_ERR_ARG, "bad argument");
+    HIP_TRY(hipSetDevice(h->device));
+    const int K = h->partitioned ? 3 : 2;
+    std::vector<hipEvent_t> ev((size_t)reps * (K + 1));
+    for (auto &e : ev) HIP_TRY(hipEventCreate(&e));
+    for (int r = 0; r < reps; r++) {
+        hipEvent_t *E = &ev[(size_t)r * (K + 1)];
+        int k = 0;
+        HIP_TRY(hipEventRecord(E[k++], h->stream));
+        if (h->partitioned) {
+            int rc = exchange(h, d_y);
+            if (rc) return rc;
+            HIP_TRY(hipEventRecord(E[k++], h->stream));
+        }
+        YView Y{d_y, h->d_gele, h->d_griv, h->n_own, h->n_own_riv};
+        launch_element_kernel(h->dm, Y, d_ydot, h->n_own + h->n_segghost, h->cur, h->cur_e, h->mode, h->open,
+                              false, h->dd, h->stream);
+        HIP_TRY(hipEventRecord(E[k++], h->stream));
+        launch_river_kernel(h->dm, Y, d_ydot, h->mode, false, h->dd, h->stream);
+        HIP_TRY(hipEventRecord(E[k++], h->stream));
+        h->last_cur = h->cur; h->last_cur_e = h->cur_e;
+        h->cur ^= 1;
+        if (h->mode == SHUD_MODE_SERIAL) h->cur_e ^= 1;
+        h->last_y = d_y; h->have_last = true; h->ncalls++;
+    }
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    std::vector<double> acc(K, 0.0);
+    double tot = 0.0;
+    for (int r = 0; r < reps; r++) {
+        hipEvent_t *E = &ev[(size_t)r * (K + 1)];
+        for (int k = 0; k < K; k++) {
+            float ms = 0.f;
+            HIP_TRY(hipEventElapsedTime(&ms, E[k], E[k + 1]));
+            acc[k] += ms;
+        }
+        float all = 0.f;
+        HIP_TRY(hipEventElapsedTime(&all, E[0], E[K]));
+        tot += all;
+    }
+    for (auto &e : ev) (void)hipEventDestroy(e);
+    const char *nm = h->partitioned ? "halo_exchange,shud_ele_kernel,shud_riv_kernel" : "shud_ele_kernel,shud_riv_kernel";
+    int n = std::min(*nk, K);
+    for (int k = 0; k < n; k++) ms_out[k] = acc[k] / reps;
+    *nk = K;
+    if (ms_eval) *ms_eval = tot / reps;
+    if (names_out && names_len > 0) snprintf(names_out, names_len, "%s", nm);
+    return SHUD_OK;
+}

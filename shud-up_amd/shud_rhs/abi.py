@@ -1,0 +1,135 @@
+"""ctypes mirror of include/shud_rhs.h (the C-ABI boundary).
+
+Struct layouts here must match the header field for field; tests/test_abi.py checks sizes and that
+libshud_rhs.so exports every function the header declares.
+"""
+import ctypes as C
+
+c_int32_p = C.POINTER(C.c_int32)
+c_double_p = C.POINTER(C.c_double)
+
+SHUD_OK = 0
+SHUD_ERR_PHYSICS = -1
+SHUD_ERR_ARG = -2
+SHUD_ERR_HIP = -3
+SHUD_ERR_NCCL = -4
+SHUD_ERR_UNSUPPORTED = -5
+
+SHUD_MODE_SERIAL = 0
+SHUD_MODE_OMP = 1
+SHUD_WHERE_HOST = 0
+SHUD_WHERE_DEVICE = 1
+
+EF_NAN_QELE = 0x01
+EF_EFFKH = 0x02
+EF_ET_NEG = 0x04
+EF_ET_NAN = 0x08
+EF_AET_WARN = 0x10
+
+MESH_FIELDS = [
+    ("num_ele", C.c_int32), ("num_riv", C.c_int32), ("num_seg", C.c_int32), ("close_boundary", C.c_int32),
+    ("nabr", c_int32_p), ("area", c_double_p), ("z_surf", c_double_p), ("z_bottom", c_double_p),
+    ("depression", c_double_p), ("edge", c_double_p), ("dist2nabor", c_double_p), ("dist2edge", c_double_p),
+    ("avg_rough", c_double_p), ("rough", c_double_p), ("ibc", c_int32_p), ("iss", c_int32_p), ("ilake", c_int32_p),
+    ("riv_down", c_int32_p), ("riv_bc", c_int32_p), ("riv_length", c_double_p), ("riv_bed_slope", c_double_p),
+    ("riv_dist2down", c_double_p), ("riv_avg_rough", c_double_p), ("riv_depth", c_double_p),
+    ("riv_bottom_width", c_double_p), ("riv_bankslope", c_double_p), ("riv_ksath", c_double_p),
+    ("riv_bedthick", c_double_p),
+    ("seg_ele", c_int32_p), ("seg_riv", c_int32_p), ("seg_length", c_double_p), ("seg_cwr", c_double_p),
+]
+PARAM_NAMES = ["aquifer_depth", "macD", "macKsatH", "geo_vAreaF", "KsatH", "KsatV", "infKsatV", "hAreaF",
+               "macKsatV", "ThetaS", "ThetaR", "Beta", "infD", "Sy", "RzD", "VegFrac", "ImpAF"]
+STEP_ARRAYS = ["net_prep", "pot_evap", "pot_tran", "etp", "lai", "fu_surf", "fu_sub", "e_ic", "u_satn",
+               "ugw_stale"]
+DIAG_ELE3 = ["qele_surf", "qele_sub"]
+DIAG_ELE = ["qele_surf_tot", "qele_sub_tot", "q_infil", "q_exfil", "q_recharge", "q_es", "q_eu", "q_eg",
+            "q_tu", "q_tg", "q_eta", "e_ic", "u_satn", "i_beta", "eff_kh", "qe2r_surf", "qe2r_sub"]
+DIAG_SEG = ["qseg_surf", "qseg_sub"]
+DIAG_RIV = ["qriv_down", "qriv_up", "qriv_surf", "qriv_sub"]
+
+
+class ShudMeshSoA(C.Structure):
+    _fields_ = MESH_FIELDS
+
+
+class ShudParamsSoA(C.Structure):
+    _fields_ = [(n, c_double_p) for n in PARAM_NAMES]
+
+
+class ShudStepInputs(C.Structure):
+    _fields_ = [(n, c_double_p) for n in STEP_ARRAYS] + [
+        ("ele_ybc", c_double_p), ("n_ele_ybc", C.c_int32),
+        ("ele_qbc", c_double_p), ("n_ele_qbc", C.c_int32),
+        ("riv_ybc", c_double_p), ("n_riv_ybc", C.c_int32),
+        ("riv_qbc", c_double_p), ("n_riv_qbc", C.c_int32),
+    ]
+
+
+class ShudRhsOptions(C.Structure):
+    _fields_ = [("mode", C.c_int32), ("device", C.c_int32), ("stream", C.c_void_p), ("check_errors", C.c_int32)]
+
+
+class ShudFluxOut(C.Structure):
+    _fields_ = [(n, c_double_p) for n in DIAG_ELE3[:2] + DIAG_ELE[:2] + ["q_infil", "q_exfil", "q_recharge",
+                                                                        "q_es", "q_eu", "q_eg", "q_tu", "q_tg",
+                                                                        "q_eta", "e_ic", "u_satn", "i_beta",
+                                                                        "eff_kh", "qe2r_surf", "qe2r_sub",
+                                                                        "qseg_surf", "qseg_sub", "qriv_down",
+                                                                        "qriv_up", "qriv_surf", "qriv_sub"]]
+
+
+FLUXOUT_ORDER = [f[0] for f in ShudFluxOut._fields_]
+
+
+class ShudErr(C.Structure):
+    _fields_ = [("flags", C.c_uint32), ("exit_code", C.c_int32), ("first_index", C.c_int32 * 8),
+                ("n_aet_warn", C.c_int64), ("message", C.c_char * 256)]
+
+
+class ShudPartition(C.Structure):
+    _fields_ = [("rank", C.c_int32), ("nranks", C.c_int32), ("n_own_ele", C.c_int32),
+                ("n_segghost_ele", C.c_int32), ("n_own_riv", C.c_int32),
+                ("ele_send_off", c_int32_p), ("ele_send_idx", c_int32_p), ("ele_recv_off", c_int32_p),
+                ("riv_send_off", c_int32_p), ("riv_send_idx", c_int32_p), ("riv_recv_off", c_int32_p),
+                ("ele_gid", c_int32_p), ("riv_gid", c_int32_p), ("nccl_unique_id", C.c_char_p)]
+
+
+# functions declared in include/shud_rhs.h (name -> (restype, argtypes))
+_H = C.c_void_p
+FUNCTIONS = {
+    "shud_rhs_abi_version": (C.c_int, []),
+    "shud_rhs_create": (C.c_int, [C.POINTER(ShudMeshSoA), C.POINTER(ShudParamsSoA), C.POINTER(ShudRhsOptions),
+                                  C.POINTER(_H)]),
+    "shud_rhs_set_step_inputs": (C.c_int, [_H, C.POINTER(ShudStepInputs)]),
+    "shud_rhs_eval": (C.c_int, [_H, C.c_double, C.c_void_p, C.c_void_p, C.c_int]),
+    "shud_rhs_sync_diagnostics": (C.c_int, [_H, C.POINTER(ShudFluxOut)]),
+    "shud_rhs_get_error": (C.c_int, [_H, C.POINTER(ShudErr)]),
+    "shud_rhs_clear_error": (C.c_int, [_H]),
+    "shud_rhs_num_calls": (C.c_longlong, [_H]),
+    "shud_rhs_destroy": (C.c_int, [_H]),
+    "shud_rhs_last_error_string": (C.c_char_p, []),
+    "shud_rhs_cvrhs": (C.c_int, [C.c_double, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "shud_rhs_device_alloc": (C.c_int, [_H, C.c_size_t, C.POINTER(C.c_void_p)]),
+    "shud_rhs_device_free": (C.c_int, [_H, C.c_void_p]),
+    "shud_rhs_memcpy": (C.c_int, [_H, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]),
+    "shud_rhs_synchronize": (C.c_int, [_H]),
+    "shud_rhs_stream": (C.c_void_p, [_H]),
+    "shud_rhs_time_kernels": (C.c_int, [_H, C.c_double, C.c_void_p, C.c_void_p, C.c_int, c_double_p, c_double_p,
+                                        C.POINTER(C.c_int), C.c_char_p, C.c_int]),
+    "shud_rhs_nccl_unique_id": (C.c_int, [C.c_char_p]),
+    "shud_rhs_create_partitioned": (C.c_int, [C.POINTER(ShudMeshSoA), C.POINTER(ShudParamsSoA),
+                                              C.POINTER(ShudRhsOptions), C.POINTER(ShudPartition),
+                                              C.POINTER(_H)]),
+    "shud_rhs_halo_buffers": (C.c_int, [_H, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                                        C.POINTER(C.c_void_p)]),
+    "shud_rhs_eval_pack": (C.c_int, [_H, C.c_void_p]),
+    "shud_rhs_eval_compute": (C.c_int, [_H, C.c_double, C.c_void_p, C.c_void_p]),
+}
+
+
+def bind(lib):
+    for name, (res, args) in FUNCTIONS.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib

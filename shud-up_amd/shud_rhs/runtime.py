@@ -1,0 +1,174 @@
+"""ctypes front end of libshud_rhs.so — the product path.  Fails loudly if the HIP library is absent.
+
+`RhsHandle` mirrors the reference call sequence: construct once from a ShudModel (Model_Data after
+initialize(), MD_initialize.cpp:168-245), `set_step_inputs` once per ET step (updateforcing()/ET(),
+MD_ET.cpp:14-342), then `eval(t, y)` per CVODE RHS call (f(), src/Model/f.cpp:2-32).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+
+_LIB = None
+LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "libshud_rhs.so")
+
+
+class ShudRhsError(RuntimeError):
+    def __init__(self, code, msg, err=None):
+        super().__init__(f"shud_rhs error {code}: {msg}")
+        self.code = code
+        self.err = err
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"HIP library {LIB_PATH} not built: run `make -C shud-up_amd` "
+                              "or __graft_entry__.build() (there is no CPU fallback)")
+        _LIB = abi.bind(C.CDLL(LIB_PATH))
+    return _LIB
+
+
+def _check(rc, what):
+    if rc != abi.SHUD_OK:
+        raise ShudRhsError(rc, f"{what}: {lib().shud_rhs_last_error_string().decode(errors='replace')}")
+
+
+class RhsHandle:
+    def __init__(self, model, mode=abi.SHUD_MODE_SERIAL, device=0, stream=None, check_errors=True,
+                 partition=None):
+        self.model = model
+        self._mesh = model.mesh_struct()
+        self._par = model.params_struct()
+        opt = abi.ShudRhsOptions(mode, device, stream, 1 if check_errors else 0)
+        h = C.c_void_p()
+        if partition is None:
+            _check(lib().shud_rhs_create(C.byref(self._mesh), C.byref(self._par), C.byref(opt), C.byref(h)),
+                   "shud_rhs_create")
+            self.n_own, self.n_own_riv = model.num_ele, model.num_riv
+        else:
+            self._part = partition.struct()
+            _check(lib().shud_rhs_create_partitioned(C.byref(self._mesh), C.byref(self._par), C.byref(opt),
+                                                     C.byref(self._part), C.byref(h)),
+                   "shud_rhs_create_partitioned")
+            self.n_own, self.n_own_riv = partition.n_own_ele, partition.n_own_riv
+        self.h = h
+        self.mode = mode
+
+    @property
+    def num_y(self):
+        return 3 * self.n_own + self.n_own_riv
+
+    def close(self):
+        if self.h:
+            lib().shud_rhs_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_step_inputs(self, step=None, bc_tables=None):
+        s = self.model.step_struct(step, bc_tables)
+        _check(lib().shud_rhs_set_step_inputs(self.h, C.byref(s)), "shud_rhs_set_step_inputs")
+
+    def eval(self, t, y, ydot=None, raise_on_physics=True):
+        """Host-array RHS: returns ydot (numpy).  Raises ShudRhsError on a physics error (the reference
+        would have exited; the error details are in .err)."""
+        y = np.ascontiguousarray(y, dtype=np.float64)
+        if y.size != self.num_y:
+            raise ValueError(f"y has {y.size} entries, expected {self.num_y}")
+        if ydot is None:
+            ydot = np.empty_like(y)
+        rc = lib().shud_rhs_eval(self.h, float(t), y.ctypes.data, ydot.ctypes.data, abi.SHUD_WHERE_HOST)
+        if rc == abi.SHUD_ERR_PHYSICS and raise_on_physics:
+            e = self.get_error()
+            raise ShudRhsError(rc, e["message"], e)
+        if rc not in (abi.SHUD_OK, abi.SHUD_ERR_PHYSICS):
+            _check(rc, "shud_rhs_eval")
+        return ydot
+
+    def eval_device(self, t, d_y, d_ydot):
+        """Stream-ordered eval on device pointers (ints)."""
+        _check(lib().shud_rhs_eval(self.h, float(t), C.c_void_p(d_y), C.c_void_p(d_ydot), abi.SHUD_WHERE_DEVICE),
+               "shud_rhs_eval(device)")
+
+    def get_error(self):
+        e = abi.ShudErr()
+        _check(lib().shud_rhs_get_error(self.h, C.byref(e)), "shud_rhs_get_error")
+        return {"flags": e.flags, "exit_code": e.exit_code, "first_index": list(e.first_index),
+                "n_aet_warn": e.n_aet_warn, "message": e.message.decode(errors="replace")}
+
+    def clear_error(self):
+        _check(lib().shud_rhs_clear_error(self.h), "shud_rhs_clear_error")
+
+    def num_calls(self):
+        return lib().shud_rhs_num_calls(self.h)
+
+    def diagnostics(self):
+        m = self.model
+        NE, NR, NS = m.num_ele, m.num_riv, m.num_seg
+        out = {}
+        o = abi.ShudFluxOut()
+        for name in abi.FLUXOUT_ORDER:
+            n = 3 * NE if name in abi.DIAG_ELE3 else NS if name in abi.DIAG_SEG else NR if name in abi.DIAG_RIV else NE
+            out[name] = np.zeros(n)
+            setattr(o, name, out[name].ctypes.data_as(abi.c_double_p))
+        _check(lib().shud_rhs_sync_diagnostics(self.h, C.byref(o)), "shud_rhs_sync_diagnostics")
+        return out
+
+    # ---- device memory helpers (bench / tests without torch) ----
+    def device_alloc(self, nbytes):
+        p = C.c_void_p()
+        _check(lib().shud_rhs_device_alloc(self.h, nbytes, C.byref(p)), "device_alloc")
+        return p.value
+
+    def device_free(self, p):
+        _check(lib().shud_rhs_device_free(self.h, C.c_void_p(p)), "device_free")
+
+    def h2d(self, dptr, arr):
+        arr = np.ascontiguousarray(arr)
+        _check(lib().shud_rhs_memcpy(self.h, C.c_void_p(dptr), arr.ctypes.data, arr.nbytes, 1), "memcpy H2D")
+
+    def d2h(self, arr, dptr):
+        _check(lib().shud_rhs_memcpy(self.h, arr.ctypes.data, C.c_void_p(dptr), arr.nbytes, 2), "memcpy D2H")
+        return arr
+
+    def synchronize(self):
+        _check(lib().shud_rhs_synchronize(self.h), "synchronize")
+
+    def stream(self):
+        return lib().shud_rhs_stream(self.h)
+
+    def time_kernels(self, t, d_y, d_ydot, reps):
+        ms_eval = C.c_double()
+        ms = (C.c_double * 8)()
+        nk = C.c_int(8)
+        names = C.create_string_buffer(256)
+        _check(lib().shud_rhs_time_kernels(self.h, float(t), C.c_void_p(d_y), C.c_void_p(d_ydot), int(reps),
+                                           C.byref(ms_eval), ms, C.byref(nk), names, 256), "time_kernels")
+        nm = names.value.decode().split(",")
+        return ms_eval.value, {nm[k]: ms[k] for k in range(nk.value)}
+
+    # ---- external-transport partition hooks ----
+    def halo_buffers(self):
+        p = [C.c_void_p() for _ in range(4)]
+        _check(lib().shud_rhs_halo_buffers(self.h, *[C.byref(x) for x in p]), "halo_buffers")
+        return [x.value for x in p]
+
+    def eval_pack(self, d_y):
+        _check(lib().shud_rhs_eval_pack(self.h, C.c_void_p(d_y)), "eval_pack")
+
+    def eval_compute(self, t, d_y, d_ydot):
+        _check(lib().shud_rhs_eval_compute(self.h, float(t), C.c_void_p(d_y), C.c_void_p(d_ydot)), "eval_compute")
+
+
+def nccl_unique_id():
+    buf = C.create_string_buffer(128)
+    _check(lib().shud_rhs_nccl_unique_id(buf), "nccl_unique_id")
+    return buf.raw

@@ -1,0 +1,167 @@
+"""GPU parity: libshud_rhs.so (HIP, gfx950) against the CPU restatement oracle on identical inputs.
+
+Tolerance |gpu - ref| <= 1e-12 |ref| + 1e-15 per state (conftest.RTOL/ATOL).  Every case
+runs several successive calls per state because the serial RHS is stateful (qEleE_IC, u_satn).
+"""
+import numpy as np
+import pytest
+
+import cases
+from conftest import assert_close
+from shud_rhs import abi, workload
+
+pytestmark = pytest.mark.gpu
+
+
+def _runtime():
+    from shud_rhs import runtime
+    return runtime
+
+
+def _compare_sequence(m, ys, mode, oracle_mod, ncalls=3, diag=True, label=""):
+    rt = _runtime()
+    g = rt.RhsHandle(m, mode=mode)
+    o = oracle_mod.OracleRhs(m, mode)
+    g.set_step_inputs()
+    o.set_step_inputs()
+    worst = 0.0
+    for si, y in enumerate(ys):
+        for c in range(ncalls):
+            ref, code, _, _ = o.eval(0.0, y)
+            assert code == 0, f"{label}: oracle exit {code}"
+            got = g.eval(0.0, y)
+            _, rel = assert_close(got, ref, what=f"{label} state {si} call {c}")
+            worst = max(worst, rel)
+    if diag:
+        dg, do = g.diagnostics(), o.diagnostics()
+        for k in abi.FLUXOUT_ORDER:
+            if mode == abi.SHUD_MODE_OMP and k in ("q_es", "q_eu", "q_eg", "q_tu", "q_tg", "q_eta", "i_beta"):
+                continue
+            assert_close(dg[k], do[k], what=f"{label} diag {k}")
+    assert g.num_calls() == len(ys) * ncalls
+    g.close()
+    return worst
+
+
+@pytest.mark.parametrize("mode", [abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP])
+def test_ccw(mode, oracle_mod):
+    m, y0 = cases.ccw()
+    _compare_sequence(m, cases.states(m, y0), mode, oracle_mod, label="ccw")
+
+
+@pytest.mark.parametrize("mode", [abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP])
+def test_heihe(mode, oracle_mod):
+    m, y0 = cases.heihe()
+    _compare_sequence(m, cases.states(m, y0), mode, oracle_mod, label="heihe")
+
+
+@pytest.mark.parametrize("mode", [abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP])
+def test_variant_branches(mode, oracle_mod):
+    m, y = cases.variant()
+    _compare_sequence(m, [y] + cases.states(m, None, 2, seed=9), mode, oracle_mod, label="variant")
+
+
+def test_step_inputs_update(oracle_mod):
+    """A new ET step (set_step_inputs) mid-sequence, carried state overridden then carried on."""
+    rt = _runtime()
+    m, y0 = cases.ccw()
+    g, o = rt.RhsHandle(m), oracle_mod.OracleRhs(m, 0)
+    g.set_step_inputs(); o.set_step_inputs()
+    y = workload.random_state(m, seed=3)
+    for step_seed in [21, 22]:
+        st = workload.random_step_inputs(m, seed=step_seed)
+        g.set_step_inputs(st); o.set_step_inputs(st)
+        for c in range(2):
+            assert_close(g.eval(1.0, y), o.eval(1.0, y)[0], what=f"step {step_seed} call {c}")
+    # partial update (NULL arrays keep the previous values)
+    st = {"net_prep": np.full(m.num_ele, 1e-5)}
+    g.set_step_inputs(st); o.set_step_inputs(st)
+    assert_close(g.eval(2.0, y), o.eval(2.0, y)[0], what="partial step update")
+
+
+def test_device_pointer_eval(oracle_mod):
+    rt = _runtime()
+    m, y0 = cases.ccw()
+    g, o = rt.RhsHandle(m), oracle_mod.OracleRhs(m, 0)
+    g.set_step_inputs(); o.set_step_inputs()
+    ny = m.num_y
+    dy_ptr, dd_ptr = g.device_alloc(8 * ny), g.device_alloc(8 * ny)
+    try:
+        for c in range(3):
+            g.h2d(dy_ptr, y0)
+            g.eval_device(0.0, dy_ptr, dd_ptr)
+            got = g.d2h(np.zeros(ny), dd_ptr)
+            assert_close(got, o.eval(0.0, y0)[0], what=f"device eval call {c}")
+        ms, per = g.time_kernels(0.0, dy_ptr, dd_ptr, 3)
+        assert ms > 0 and per["shud_ele_kernel"] > 0
+    finally:
+        g.device_free(dy_ptr)
+        g.device_free(dd_ptr)
+
+
+def test_cvrhs_entry(oracle_mod):
+    """shud_rhs_cvrhs: the CVRhsFn body (user_data = handle) used by the INTEGRATION.md adapter."""
+    import ctypes as C
+    rt = _runtime()
+    m, y0 = cases.ccw()
+    g, o = rt.RhsHandle(m), oracle_mod.OracleRhs(m, 0)
+    g.set_step_inputs(); o.set_step_inputs()
+    dy = np.zeros(m.num_y)
+    rc = rt.lib().shud_rhs_cvrhs(0.0, y0.ctypes.data, dy.ctypes.data, g.h)
+    assert rc == 0
+    assert_close(dy, o.eval(0.0, y0)[0], what="cvrhs")
+
+
+@pytest.mark.parametrize("kind", ["et_negative", "effkh", "nan"])
+def test_error_paths(kind, oracle_mod):
+    """Where the reference would myexit(), the GPU reports the same exit code and element."""
+    rt = _runtime()
+    m, y0 = cases.ccw()
+    y = y0.copy()
+    if kind == "et_negative":
+        m.step["pot_evap"][[700, 300]] = -1e-3          # CheckNonNegative(Es) -> exit 10
+        m.step["lai"][:] = 0.0
+        y[300] = 0.01
+        y[700] = 0.01
+    elif kind == "effkh":
+        m.par["macKsatH"][[900, 400]] = 1e15           # effKH > 1e9 -> exit 13
+        aq = m.par["aquifer_depth"]
+        for i in (900, 400):
+            y[2 * m.num_ele + i] = aq[i] - 0.5 * m.par["macD"][i]
+    else:
+        y[2 * m.num_ele + 500] = np.nan                 # NaN groundwater -> CheckNANij -> exit 10
+    g, o = rt.RhsHandle(m), oracle_mod.OracleRhs(m, 0)
+    g.set_step_inputs(); o.set_step_inputs()
+    _, code, idx, _ = o.eval(0.0, y)
+    assert code in (10, 13)
+    with pytest.raises(rt.ShudRhsError) as ei:
+        g.eval(0.0, y)
+    e = ei.value.err
+    assert e["exit_code"] == code
+    fi = e["first_index"]
+    if kind == "et_negative":
+        assert min(v for v in (fi[2], fi[3]) if v >= 0) == idx
+    elif kind == "effkh":
+        assert fi[1] == idx
+    else:
+        assert fi[0] == idx
+
+
+def test_lake_rejected():
+    rt = _runtime()
+    m, _ = cases.ccw()
+    m.ilake = np.zeros(m.num_ele, dtype=np.int32)
+    m.ilake[5] = 1
+    with pytest.raises(rt.ShudRhsError) as ei:
+        rt.RhsHandle(m)
+    assert ei.value.code == abi.SHUD_ERR_UNSUPPORTED
+
+
+@pytest.mark.parametrize("mode", [abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP])
+def test_syn_1m(mode, oracle_mod):
+    """syn-1M: full-size parity against the oracle, 2 successive calls."""
+    from shud_rhs import synth
+    m = synth.synth_model(1_000_000)
+    m.step = workload.random_step_inputs(m)
+    y = workload.random_state(m)
+    _compare_sequence(m, [y], mode, oracle_mod, ncalls=2, diag=False, label="syn-1M")
