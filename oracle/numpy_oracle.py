@@ -7,7 +7,35 @@ Same fp64 operation order as the reference, so on identical inputs it must agree
 bit for bit.  Citations are to /root/reference/src.  Serial (`make shud`) and OMP semantics.
 Pure-numpy; sized for meshes up to ~1e5 elements in tests.
 """
+import ctypes
+import ctypes.util
+
 import numpy as np
+
+# glibc libm (the library the reference links): numpy's SIMD cbrt/power/cos differ by an ulp
+_libm = ctypes.CDLL(ctypes.util.find_library("m") or "libm.so.6")
+for _f in ("cbrt", "cos"):
+    getattr(_libm, _f).restype = ctypes.c_double
+    getattr(_libm, _f).argtypes = [ctypes.c_double]
+_libm.pow.restype = ctypes.c_double
+_libm.pow.argtypes = [ctypes.c_double, ctypes.c_double]
+_vcbrt = np.vectorize(_libm.cbrt, otypes=[np.float64])
+_vcos = np.vectorize(_libm.cos, otypes=[np.float64])
+_vpow = np.vectorize(_libm.pow, otypes=[np.float64])
+
+
+def cbrt(x):
+    return _vcbrt(np.asarray(x, dtype=np.float64))
+
+
+def cos(x):
+    return _vcos(np.asarray(x, dtype=np.float64))
+
+
+def power(a, b):
+    a, b = np.broadcast_arrays(np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64))
+    return _vpow(a, b)
+
 
 ZERO = 1.0e-10
 EPSILON = 0.005
@@ -25,7 +53,7 @@ def rmax(a, b):          # functions.hpp:120-123
 
 
 def manning(A, n, R, S):  # Equations.hpp:54-63, pow23 :36-39
-    t = np.cbrt(R)
+    t = cbrt(R)
     p23 = t * t
     with np.errstate(invalid="ignore", divide="ignore"):
         pos = np.sqrt(np.where(S > 0, S, 0.0)) * A * p23 / n
@@ -100,7 +128,7 @@ class NumpyRhs:
             pet, ptr, eic = st["pot_evap"], st["pot_tran"], self.e_ic.copy()
             fc = ThS * 0.75
             b = rmin(rmax(0.0, (self.u_satn * (ThS - ThR) - ThR) / (fc - ThR)), 1.0)
-            beta = 0.5 * (1 - np.cos(PI * b))
+            beta = 0.5 * (1 - cos(PI * b))
             Es = rmin(rmax(0.0, ysf), pet) * vb
             wet = ugw > aq - infD
             Eg = np.where((Es < pet) & wet, rmin(rmax(0.0, ugw), pet - Es) * pj * vb, 0.0)
@@ -129,7 +157,7 @@ class NumpyRhs:
             hi, lo = satn > 0.99, satn <= ZERO
             n = P["Beta"]
             s_ = np.where(hi | lo, 0.5, satn)
-            tmp = -1.0 + np.power(1.0 - np.power(s_, n / (n - 1.0)), (n - 1.0) / n)
+            tmp = -1.0 + power(1.0 - power(s_, n / (n - 1.0)), (n - 1.0) / n)
             satkr = np.where(hi, 1.0, np.where(lo, 0.0, np.sqrt(s_) * tmp * tmp))
             theta = np.where(hi, ThS, np.where(lo, ThR, theta))
             satn = np.where(hi, 1.0, np.where(lo, 0.0, satn))
@@ -187,7 +215,7 @@ class NumpyRhs:
                 with np.errstate(invalid="ignore", divide="ignore"):
                     sb = isf / d2e * 0.5
                     qb_s = np.where((isf > dep) & (sb > 0.0),
-                                    np.sqrt(np.where(sb > 0, sb, 0.0)) * np.cbrt(isf * isf * isf * isf * isf) * B / E["rough"], 0.0)
+                                    np.sqrt(np.where(sb > 0, sb, 0.0)) * cbrt(isf * isf * isf * isf * isf) * B / E["rough"], 0.0)
                     gb = ugw / d2e * 0.5
                     qb_g = np.where((ugw > dep * 10.0) & (gb > 0.0), ekh * gb, 0.0)
             QS[j] = np.where(has, q, qb_s)

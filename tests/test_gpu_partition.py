@@ -1,0 +1,67 @@
+"""GPU: partitioned handles (owned + ghost entities) on one MI355X, halo moved between the
+handles' device buffers by the test (external transport: shud_rhs_eval_pack -> D2D copies ->
+shud_rhs_eval_compute).  Owned DY must be bit-identical to the single-GPU handle's.  The RCCL transport
+used by bench.py at N > 1 replaces only the D2D copies (grouped ncclSend/ncclRecv of the same ranges)."""
+import numpy as np
+import pytest
+
+import cases
+from shud_rhs import partition, workload
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_partitioned_handles_bit_identical(nranks, mode):
+    from shud_rhs import runtime as rt
+    m, y = cases.variant(20000, seed=17)
+    single = rt.RhsHandle(m, mode=mode)
+    single.set_step_inputs()
+    _, _, plans = partition.build_plans(m, nranks)
+    locs = [partition.local_model(m, plans[r], r, nranks) for r in range(nranks)]
+    hs, bufs, halos = [], [], []
+    for lm, part in locs:
+        h = rt.RhsHandle(lm, mode=mode, partition=part)
+        h.set_step_inputs()
+        hs.append(h)
+        ny = 3 * part.n_own_ele + part.n_own_riv
+        bufs.append((h.device_alloc(8 * ny), h.device_alloc(8 * ny), ny))
+        halos.append(h.halo_buffers())
+    try:
+        for yy in [y, workload.random_state(m, seed=2)]:
+            for call in range(3):
+                ref = single.eval(0.0, yy)
+                for r, (lm, part) in enumerate(locs):
+                    hs[r].h2d(bufs[r][0], partition.local_state(yy, m, part))
+                    hs[r].eval_pack(bufs[r][0])
+                    hs[r].synchronize()
+                for r, (lm, part) in enumerate(locs):        # the all-to-all-v, as D2D copies
+                    _, _, gele, griv = halos[r]
+                    for p in range(nranks):
+                        if p == r:
+                            continue
+                        esend, rsend, _, _ = halos[p]
+                        pp = locs[p][1]
+                        s0, s1 = int(pp.ele_send_off[r]), int(pp.ele_send_off[r + 1])
+                        d0 = int(part.ele_recv_off[p])
+                        if s1 > s0:
+                            import ctypes as C
+                            rt.lib().shud_rhs_memcpy(hs[r].h, C.c_void_p(gele + 24 * d0), C.c_void_p(esend + 24 * s0),
+                                                     24 * (s1 - s0), 3)
+                        s0, s1 = int(pp.riv_send_off[r]), int(pp.riv_send_off[r + 1])
+                        d0 = int(part.riv_recv_off[p])
+                        if s1 > s0:
+                            import ctypes as C
+                            rt.lib().shud_rhs_memcpy(hs[r].h, C.c_void_p(griv + 8 * d0), C.c_void_p(rsend + 8 * s0),
+                                                     8 * (s1 - s0), 3)
+                for r, (lm, part) in enumerate(locs):
+                    hs[r].eval_compute(0.0, bufs[r][0], bufs[r][1])
+                    got = hs[r].d2h(np.zeros(bufs[r][2]), bufs[r][1])
+                    want = partition.local_state(ref, m, part)
+                    assert np.array_equal(got, want), f"rank {r} call {call}: {(got != want).sum()} differ"
+    finally:
+        for h, (a, b, _) in zip(hs, bufs):
+            h.device_free(a)
+            h.device_free(b)
+            h.close()
