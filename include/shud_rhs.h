@@ -165,6 +165,9 @@ int  shud_rhs_sync_diagnostics(shud_rhs_t h, ShudFluxOut *out);
 int  shud_rhs_get_error(shud_rhs_t h, ShudErr *err);
 int  shud_rhs_clear_error(shud_rhs_t h);
 long long shud_rhs_num_calls(shud_rhs_t h);  /* Model_Data::nFCall */
+/* device layout chosen at create: *packed = 1 when per-element parameters were folded into
+ * *n_classes distinct parameter tuples (the fast element kernel); 0 = plain SoA kernel */
+int  shud_rhs_layout(shud_rhs_t h, int *packed, int *n_classes);
 int  shud_rhs_destroy(shud_rhs_t h);
 const char *shud_rhs_last_error_string(void);
 

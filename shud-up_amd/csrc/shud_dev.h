@@ -38,6 +38,43 @@ struct DevMesh {
     DevErr *err;
 };
 
+// ---- packed "class" layout (built by shud_rhs_create when the mesh allows it) -----------------------
+// Per-element hydraulic parameters of a SHUD model are copies of a few soil/geol/landcover rows
+// (_Element::copySoil/copyGeol/copyLandc, Element.cpp:386-418); the handle finds the distinct
+// parameter tuples once and stores a class id per element, and interleaves the element's own streams
+// into 16-byte records so one lane issues a few wide loads instead of ~45 narrow ones.  Pure layout:
+// every value the kernel computes with is bit-identical to the SoA input.
+struct ClassRec {
+    double macD, macKsatH, vAreaF, KsatH, KsatV, infKsatV, hAreaF, macKsatV;
+    double ThetaS, ThetaR, Beta, infD, Sy, RzD, VegFrac, ImpAF, depression, rough;
+    // per-class subexpressions, evaluated once on the host with the reference's own operation order
+    // (so they are the same doubles the per-element code would produce)
+    double bexp1;    // n / (n - 1.)            satKfun, Equations.cpp:137
+    double bexp2;    // (n - 1.) / n            satKfun, Equations.cpp:137
+    double ths_thr;  // ThetaS - ThetaR         Element.cpp:363, is_sm_et.cpp:133
+    double fc_thr;   // ThetaS * 0.75 - ThetaR  is_sm_et.cpp:133, Element.cpp:314 (ThetaFC - ThetaR)
+    double kmax;     // infKsatV*(1-hAreaF) + macKsatV*hAreaF   Element.cpp:351
+    double omh;      // 1 - hAreaF
+    double hamac;    // hAreaF * macKsatV       Element.cpp:286-288
+    double vb;       // 1 - VegFrac             MD_ET.cpp:345
+    double pj;       // 1 - ImpAF               MD_ET.cpp:346
+};
+struct DevPacked {
+    const ClassRec *cls;
+    const double2 *zz;      // {z_surf, z_bottom}                      (also gathered by neighbours)
+    const double2 *aqk;     // {aquifer_depth, bits = class << 32 | flags}  (also gathered by neighbours)
+    const int4 *meta;       // {nabr0, nabr1, nabr2, first segment (element-sorted)}
+    const double2 *ge01;    // {edge0, edge1}
+    const double2 *ge2a;    // {edge2, area}
+    const double2 *gd01;    // {dist2nabor0, dist2nabor1}
+    const double *gd2;      // dist2nabor2
+    double2 *s_np;          // {net_prep, pot_evap}        step inputs (packed by shud_pack_step_kernel)
+    double2 *s_tl;          // {pot_tran, lai}
+    double2 *s_fu;          // {fu_surf, fu_sub}            read only when not all ones
+    double2 *cs[2];         // carried {u_satn, qEleE_IC}, ping-pong
+};
+// packed flags word: bits 0-15 iBC (int16), 16-17 iSS class, 18-23 number of river segments
+
 struct DevDiag {                     // optional diagnostic outputs (ShudFluxOut), local numbering
     double *qele_surf, *qele_sub, *qele_surf_tot, *qele_sub_tot, *q_infil, *q_exfil, *q_recharge;
     double *q_es, *q_eu, *q_eg, *q_tu, *q_tg, *q_eta, *e_ic, *u_satn, *i_beta, *eff_kh;
@@ -59,7 +96,11 @@ struct YView {
 };
 
 void launch_element_kernel(const DevMesh &m, const YView &Y, double *dy, int n_compute, int cur, int cur_e,
-                           int mode, bool open, bool diag, const DevDiag &dg, hipStream_t s);
+                           int mode, bool open, bool diag, const DevDiag &dg, hipStream_t s, int variant = 0);
+void launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int n_compute,
+                                  int cur, int mode, bool open, bool diag, bool fu_unit, const DevDiag &dg,
+                                  hipStream_t s, int pk_waves = 0);
+void launch_pack_step_kernel(const DevMesh &m, const DevPacked &p, int n, int cur, unsigned what, hipStream_t s);
 void launch_river_kernel(const DevMesh &m, const YView &Y, double *dy, int mode, bool diag,
                          const DevDiag &dg, hipStream_t s);
 void launch_pack_kernel(const double *y, int n_own, int n_own_riv, const int *eidx, int ne, const int *ridx,

@@ -20,6 +20,7 @@
 #include <cstring>
 #include <numeric>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "shud_dev.h"
@@ -73,6 +74,12 @@ struct shud_rhs {
     bool have_diag = false;
     int cur = 0, cur_e = 0;
     long long ncalls = 0;
+    int variant = 0;                     // element-kernel build variant (SHUD_RHS_ELE_VARIANT, A/B only)
+    bool packed = false;                 // class-table / 16-byte-record layout in use (DevPacked)
+    int pk_waves = 0;                    // SHUD_RHS_PK_WAVES (A/B only)
+    DevPacked dp{};
+    int n_classes = 0;
+    bool fu_unit[2] = {true, true};      // fu_Surf / fu_Sub are all 1.0 (cryosphere off): not read
 
     // host-pointer eval staging
     double *d_y = nullptr, *d_ydot = nullptr, *d_scratch_dy = nullptr;
@@ -141,6 +148,9 @@ extern "C" const char *shud_rhs_last_error_string(void) { return g_last_error.c_
 // ---------------------------------------------------------------------------------------------
 // create
 // ---------------------------------------------------------------------------------------------
+static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, const std::vector<int> &eflags,
+                        const std::vector<int> &seg_off);
+
 static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, const ShudRhsOptions *opt,
                  const ShudPartition *part) {
     const int NE = m->num_ele, NR = m->num_riv, NS = m->num_seg;
@@ -154,6 +164,8 @@ static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, cons
     h->n_own = part ? part->n_own_ele : NE;
     h->n_segghost = part ? part->n_segghost_ele : 0;
     h->n_own_riv = part ? part->n_own_riv : NR;
+    if (const char *v = getenv("SHUD_RHS_ELE_VARIANT")) h->variant = atoi(v);
+    if (const char *v = getenv("SHUD_RHS_PK_WAVES")) h->pk_waves = atoi(v);
     if (h->n_own < 0 || h->n_own + h->n_segghost > NE || h->n_own_riv < 0 || h->n_own_riv > NR)
         return fail(SHUD_ERR_ARG, "partition counts inconsistent with mesh sizes");
 
@@ -332,6 +344,7 @@ static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, cons
         UP(rseg_off, rseg_off.data(), rseg_off.size()); UP(rseg_pos, rseg_pos.data(), rseg_pos.size());
     }
 #undef UP
+    if ((rc = build_packed(h, m, p, eflags, seg_off))) return rc;
     if ((rc = h->dalloc(&h->d_err, 1))) return rc;
     d.err = h->d_err;
     HIP_TRY(hipHostMalloc((void **)&h->h_err, sizeof(DevErr), hipHostMallocDefault));
@@ -340,6 +353,98 @@ static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, cons
     if ((rc = h->dalloc(&h->d_y, ny))) return rc;
     if ((rc = h->dalloc(&h->d_ydot, ny))) return rc;
     if ((rc = h->dalloc(&h->d_scratch_dy, ny))) return rc;
+    return 0;
+}
+
+// Packed class layout (shud_dev.h DevPacked).  Returns 0 with h->packed set, 0 with h->packed clear when
+// the mesh does not qualify (the SoA kernel is used), or an error code.
+static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, const std::vector<int> &eflags,
+                        const std::vector<int> &seg_off) {
+    const char *env = getenv("SHUD_RHS_PACKED");
+    if ((env && env[0] == '0') || h->variant) return 0;
+    const int NE = m->num_ele;
+    if (!m->rough || NE == 0) return 0;
+    // avgRough must be the reference's 0.5*(Rough_i + Rough_nabr) / Rough_i (Element.cpp:249-265)
+    for (int j = 0; j < 3; j++)
+        for (int i = 0; i < NE; i++) {
+            const int nb = m->nabr[(size_t)j * NE + i];
+            const double want = nb >= 0 ? 0.5 * (m->rough[i] + m->rough[nb]) : m->rough[i];
+            if (!(m->avg_rough[(size_t)j * NE + i] == want)) return 0;
+        }
+    for (int i = 0; i < NE; i++)
+        if (seg_off[i + 1] - seg_off[i] > 63) return 0;
+    // distinct parameter tuples -> class ids
+    std::vector<ClassRec> table;
+    std::vector<int> cls(NE);
+    struct Key { std::string b; bool operator==(const Key &o) const { return b == o.b; } };
+    struct KH { size_t operator()(const Key &k) const { return std::hash<std::string>()(k.b); } };
+    std::unordered_map<Key, int, KH> ids;
+    const double dep_default = 0.0002;
+    for (int i = 0; i < NE; i++) {
+        ClassRec r;
+        r.macD = p->macD[i]; r.macKsatH = p->macKsatH[i]; r.vAreaF = p->geo_vAreaF[i]; r.KsatH = p->KsatH[i];
+        r.KsatV = p->KsatV[i]; r.infKsatV = p->infKsatV[i]; r.hAreaF = p->hAreaF[i]; r.macKsatV = p->macKsatV[i];
+        r.ThetaS = p->ThetaS[i]; r.ThetaR = p->ThetaR[i]; r.Beta = p->Beta[i]; r.infD = p->infD[i]; r.Sy = p->Sy[i];
+        r.RzD = p->RzD[i]; r.VegFrac = p->VegFrac[i]; r.ImpAF = p->ImpAF[i];
+        r.depression = m->depression ? m->depression[i] : dep_default;
+        r.rough = m->rough[i];
+        const double n = r.Beta;
+        r.bexp1 = n / (n - 1.);
+        r.bexp2 = (n - 1.) / n;
+        r.ths_thr = r.ThetaS - r.ThetaR;
+        r.fc_thr = r.ThetaS * 0.75 - r.ThetaR;
+        r.kmax = r.infKsatV * (1. - r.hAreaF) + r.macKsatV * r.hAreaF;
+        r.omh = 1 - r.hAreaF;
+        r.hamac = r.hAreaF * r.macKsatV;
+        r.vb = 1. - r.VegFrac;
+        r.pj = 1. - r.ImpAF;
+        Key k{std::string((const char *)&r, sizeof(r))};
+        auto it = ids.find(k);
+        if (it == ids.end()) {
+            if ((int)table.size() >= (1 << 20)) return 0;
+            it = ids.emplace(k, (int)table.size()).first;
+            table.push_back(r);
+        }
+        cls[i] = it->second;
+    }
+    std::vector<double2> zz(NE), aqk(NE), e01(NE), e2a(NE), d01(NE);
+    std::vector<double> d2(NE);
+    std::vector<int4> meta(NE);
+    for (int i = 0; i < NE; i++) {
+        zz[i] = make_double2(m->z_surf[i], m->z_bottom[i]);
+        const int nseg = seg_off[i + 1] - seg_off[i];
+        const unsigned fl = (unsigned)(eflags[i] & 0x3ffff) | ((unsigned)nseg << 18);
+        const unsigned long long bits = ((unsigned long long)(unsigned)cls[i] << 32) | fl;
+        double bd;
+        memcpy(&bd, &bits, 8);
+        aqk[i] = make_double2(p->aquifer_depth[i], bd);
+        meta[i] = make_int4(m->nabr[i], m->nabr[(size_t)NE + i], m->nabr[2 * (size_t)NE + i], seg_off[i]);
+        e01[i] = make_double2(m->edge[i], m->edge[(size_t)NE + i]);
+        e2a[i] = make_double2(m->edge[2 * (size_t)NE + i], m->area[i]);
+        d01[i] = make_double2(m->dist2nabor[i], m->dist2nabor[(size_t)NE + i]);
+        d2[i] = m->dist2nabor[2 * (size_t)NE + i];
+    }
+    int rc;
+    DevPacked &P = h->dp;
+    ClassRec *cls_d; double2 *zz_d, *aqk_d, *e01_d, *e2a_d, *d01_d; double *d2_d; int4 *meta_d;
+    if ((rc = h->upload(&cls_d, table.data(), table.size()))) return rc;
+    if ((rc = h->upload(&zz_d, zz.data(), NE))) return rc;
+    if ((rc = h->upload(&aqk_d, aqk.data(), NE))) return rc;
+    if ((rc = h->upload(&meta_d, meta.data(), NE))) return rc;
+    if ((rc = h->upload(&e01_d, e01.data(), NE))) return rc;
+    if ((rc = h->upload(&e2a_d, e2a.data(), NE))) return rc;
+    if ((rc = h->upload(&d01_d, d01.data(), NE))) return rc;
+    if ((rc = h->upload(&d2_d, d2.data(), NE))) return rc;
+    P.cls = cls_d; P.zz = zz_d; P.aqk = aqk_d; P.meta = meta_d; P.ge01 = e01_d; P.ge2a = e2a_d; P.gd01 = d01_d;
+    P.gd2 = d2_d;
+    if ((rc = h->upload(&P.s_np, (const double2 *)nullptr, NE))) return rc;
+    if ((rc = h->upload(&P.s_tl, (const double2 *)nullptr, NE))) return rc;
+    if ((rc = h->upload(&P.cs[0], (const double2 *)nullptr, NE))) return rc;
+    if ((rc = h->upload(&P.cs[1], (const double2 *)nullptr, NE))) return rc;
+    std::vector<double2> ones(NE, make_double2(1.0, 1.0));
+    if ((rc = h->upload(&P.s_fu, ones.data(), NE))) return rc;
+    h->n_classes = (int)table.size();
+    h->packed = true;
     return 0;
 }
 
@@ -432,12 +537,32 @@ extern "C" int shud_rhs_set_step_inputs(shud_rhs_t h, const ShudStepInputs *in) 
     if (!h || !in) return fail(SHUD_ERR_ARG, "null argument");
     HIP_TRY(hipSetDevice(h->device));
     const size_t nb = (size_t)h->NE * sizeof(double);
+    // packed layout: carried-state overrides go through SoA staging slot 0, then into the packed record
+    const double *eic_dst = h->packed ? h->dm.e_ic[0] : h->dm.e_ic[h->cur_e];
+    const double *satn_dst = h->packed ? h->dm.u_satn[0] : h->dm.u_satn[h->cur];
     struct { const double *src; const double *dst; } arr[] = {
         {in->net_prep, h->dm.net_prep}, {in->pot_evap, h->dm.pot_evap}, {in->pot_tran, h->dm.pot_tran},
         {in->etp, h->dm.etp}, {in->lai, h->dm.lai}, {in->fu_surf, h->dm.fu_surf}, {in->fu_sub, h->dm.fu_sub},
-        {in->ugw_stale, h->dm.ugw_stale}, {in->e_ic, h->dm.e_ic[h->cur_e]}, {in->u_satn, h->dm.u_satn[h->cur]}};
+        {in->ugw_stale, h->dm.ugw_stale}, {in->e_ic, eic_dst}, {in->u_satn, satn_dst}};
     for (auto &a : arr)
         if (a.src) HIP_TRY(hipMemcpyAsync((void *)a.dst, a.src, nb, hipMemcpyHostToDevice, h->stream));
+    if (h->packed) {
+        auto all_ones = [&](const double *v) {
+            for (int i = 0; i < h->NE; i++)
+                if (!(v[i] == 1.0)) return false;
+            return true;
+        };
+        if (in->fu_surf) h->fu_unit[0] = all_ones(in->fu_surf);
+        if (in->fu_sub) h->fu_unit[1] = all_ones(in->fu_sub);
+        unsigned what = 0;
+        if (in->net_prep || in->pot_evap) what |= 1;
+        if (in->pot_tran || in->lai) what |= 2;
+        if (in->fu_surf || in->fu_sub) what |= 4;
+        if (in->u_satn) what |= 8;
+        if (in->e_ic) what |= 16;
+        launch_pack_step_kernel(h->dm, h->dp, h->NE, h->cur, what, h->stream);
+        HIP_TRY(hipGetLastError());
+    }
     const double *tabs[4] = {in->ele_ybc, in->ele_qbc, in->riv_ybc, in->riv_qbc};
     const int ns[4] = {in->n_ele_ybc, in->n_ele_qbc, in->n_riv_ybc, in->n_riv_qbc};
     for (int k = 0; k < 4; k++) {
@@ -474,11 +599,28 @@ static int exchange(shud_rhs *h, const double *y) {
     return 0;
 }
 
-static void launch_all(shud_rhs *h, const double *y, double *dy, int cur, int cur_e, bool diag) {
+static void launch_ele(shud_rhs *h, const double *y, double *dy, int cur, int cur_e, bool diag) {
     YView Y{y, h->d_gele, h->d_griv, h->n_own, h->n_own_riv};
-    launch_element_kernel(h->dm, Y, dy, h->n_own + h->n_segghost, cur, cur_e, h->mode, h->open, diag, h->dd,
-                          h->stream);
+    if (h->packed && !h->variant)
+        launch_element_kernel_packed(h->dm, h->dp, Y, dy, h->n_own + h->n_segghost, cur, h->mode, h->open, diag,
+                                     h->fu_unit[0] && h->fu_unit[1], h->dd, h->stream, h->pk_waves);
+    else
+        launch_element_kernel(h->dm, Y, dy, h->n_own + h->n_segghost, cur, cur_e, h->mode, h->open, diag, h->dd,
+                              h->stream, h->variant);
+}
+static void launch_riv(shud_rhs *h, const double *y, double *dy, bool diag) {
+    YView Y{y, h->d_gele, h->d_griv, h->n_own, h->n_own_riv};
     launch_river_kernel(h->dm, Y, dy, h->mode, diag, h->dd, h->stream);
+}
+static void launch_all(shud_rhs *h, const double *y, double *dy, int cur, int cur_e, bool diag) {
+    launch_ele(h, y, dy, cur, cur_e, diag);
+    launch_riv(h, y, dy, diag);
+}
+// carried-state ping-pong after an eval: the packed record carries {u_satn, e_ic} together
+static void flip(shud_rhs *h) {
+    h->cur ^= 1;
+    if (h->packed && !h->variant) h->cur_e = h->cur;
+    else if (h->mode == SHUD_MODE_SERIAL) h->cur_e ^= 1;
 }
 
 static int read_err(shud_rhs *h) {
@@ -497,8 +639,7 @@ static int eval_device(shud_rhs *h, double t, const double *y, double *dy) {
     h->last_cur_e = h->cur_e;
     launch_all(h, y, dy, h->cur, h->cur_e, false);
     HIP_TRY(hipGetLastError());
-    h->cur ^= 1;
-    if (h->mode == SHUD_MODE_SERIAL) h->cur_e ^= 1;
+    flip(h);
     h->last_y = y;
     h->have_last = true;
     h->ncalls++;
@@ -525,6 +666,13 @@ extern "C" int shud_rhs_eval(shud_rhs_t h, double t, const double *y, double *yd
 }
 
 extern "C" long long shud_rhs_num_calls(shud_rhs_t h) { return h ? h->ncalls : -1; }
+
+extern "C" int shud_rhs_layout(shud_rhs_t h, int *packed, int *n_classes) {
+    if (!h) return fail(SHUD_ERR_ARG, "null argument");
+    if (packed) *packed = h->packed ? 1 : 0;
+    if (n_classes) *n_classes = h->n_classes;
+    return SHUD_OK;
+}
 
 // ---------------------------------------------------------------------------------------------
 // errors
@@ -693,8 +841,7 @@ extern "C" int shud_rhs_eval_compute(shud_rhs_t h, double t, const double *d_y, 
     h->last_cur_e = h->cur_e;
     launch_all(h, d_y, d_ydot, h->cur, h->cur_e, false);
     HIP_TRY(hipGetLastError());
-    h->cur ^= 1;
-    if (h->mode == SHUD_MODE_SERIAL) h->cur_e ^= 1;
+    flip(h);
     h->last_y = d_y;
     h->have_last = true;
     h->ncalls++;
@@ -718,15 +865,12 @@ extern "C" int shud_rhs_time_kernels(shud_rhs_t h, double t, const double *d_y, 
             if (rc) return rc;
             HIP_TRY(hipEventRecord(E[k++], h->stream));
         }
-        YView Y{d_y, h->d_gele, h->d_griv, h->n_own, h->n_own_riv};
-        launch_element_kernel(h->dm, Y, d_ydot, h->n_own + h->n_segghost, h->cur, h->cur_e, h->mode, h->open,
-                              false, h->dd, h->stream);
+        launch_ele(h, d_y, d_ydot, h->cur, h->cur_e, false);
         HIP_TRY(hipEventRecord(E[k++], h->stream));
-        launch_river_kernel(h->dm, Y, d_ydot, h->mode, false, h->dd, h->stream);
+        launch_riv(h, d_y, d_ydot, false);
         HIP_TRY(hipEventRecord(E[k++], h->stream));
         h->last_cur = h->cur; h->last_cur_e = h->cur_e;
-        h->cur ^= 1;
-        if (h->mode == SHUD_MODE_SERIAL) h->cur_e ^= 1;
+        flip(h);
         h->last_y = d_y; h->have_last = true; h->ncalls++;
     }
     HIP_TRY(hipStreamSynchronize(h->stream));

@@ -110,6 +110,11 @@ class RhsHandle:
     def num_calls(self):
         return lib().shud_rhs_num_calls(self.h)
 
+    def layout(self):
+        pk, nc = C.c_int(), C.c_int()
+        _check(lib().shud_rhs_layout(self.h, C.byref(pk), C.byref(nc)), "shud_rhs_layout")
+        return {"packed": bool(pk.value), "n_classes": nc.value}
+
     def diagnostics(self):
         m = self.model
         NE, NR, NS = m.num_ele, m.num_riv, m.num_seg

@@ -18,9 +18,19 @@ def _runtime():
     return runtime
 
 
-def _compare_sequence(m, ys, mode, oracle_mod, ncalls=3, diag=True, label=""):
+@pytest.fixture(params=["packed", "soa"])
+def layout(request, monkeypatch):
+    """Both device layouts: the packed class-table kernel (default when the mesh qualifies) and the plain
+    SoA kernel (SHUD_RHS_PACKED=0)."""
+    monkeypatch.setenv("SHUD_RHS_PACKED", "1" if request.param == "packed" else "0")
+    return request.param
+
+
+def _compare_sequence(m, ys, mode, oracle_mod, ncalls=3, diag=True, label="", layout=None):
     rt = _runtime()
     g = rt.RhsHandle(m, mode=mode)
+    if layout is not None:
+        assert g.layout()["packed"] == (layout == "packed"), g.layout()
     o = oracle_mod.OracleRhs(m, mode)
     g.set_step_inputs()
     o.set_step_inputs()
@@ -44,24 +54,24 @@ def _compare_sequence(m, ys, mode, oracle_mod, ncalls=3, diag=True, label=""):
 
 
 @pytest.mark.parametrize("mode", [abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP])
-def test_ccw(mode, oracle_mod):
+def test_ccw(mode, oracle_mod, layout):
     m, y0 = cases.ccw()
-    _compare_sequence(m, cases.states(m, y0), mode, oracle_mod, label="ccw")
+    _compare_sequence(m, cases.states(m, y0), mode, oracle_mod, label="ccw", layout=layout)
 
 
 @pytest.mark.parametrize("mode", [abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP])
-def test_heihe(mode, oracle_mod):
+def test_heihe(mode, oracle_mod, layout):
     m, y0 = cases.heihe()
-    _compare_sequence(m, cases.states(m, y0), mode, oracle_mod, label="heihe")
+    _compare_sequence(m, cases.states(m, y0), mode, oracle_mod, label="heihe", layout=layout)
 
 
 @pytest.mark.parametrize("mode", [abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP])
-def test_variant_branches(mode, oracle_mod):
+def test_variant_branches(mode, oracle_mod, layout):
     m, y = cases.variant()
-    _compare_sequence(m, [y] + cases.states(m, None, 2, seed=9), mode, oracle_mod, label="variant")
+    _compare_sequence(m, [y] + cases.states(m, None, 2, seed=9), mode, oracle_mod, label="variant", layout=layout)
 
 
-def test_step_inputs_update(oracle_mod):
+def test_step_inputs_update(oracle_mod, layout):
     """A new ET step (set_step_inputs) mid-sequence, carried state overridden then carried on."""
     rt = _runtime()
     m, y0 = cases.ccw()
@@ -79,7 +89,7 @@ def test_step_inputs_update(oracle_mod):
     assert_close(g.eval(2.0, y), o.eval(2.0, y)[0], what="partial step update")
 
 
-def test_device_pointer_eval(oracle_mod):
+def test_device_pointer_eval(oracle_mod, layout):
     rt = _runtime()
     m, y0 = cases.ccw()
     g, o = rt.RhsHandle(m), oracle_mod.OracleRhs(m, 0)
@@ -113,7 +123,7 @@ def test_cvrhs_entry(oracle_mod):
 
 
 @pytest.mark.parametrize("kind", ["et_negative", "effkh", "nan"])
-def test_error_paths(kind, oracle_mod):
+def test_error_paths(kind, oracle_mod, layout):
     """Where the reference would myexit(), the GPU reports the same exit code and element."""
     rt = _runtime()
     m, y0 = cases.ccw()
@@ -158,10 +168,24 @@ def test_lake_rejected():
 
 
 @pytest.mark.parametrize("mode", [abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP])
-def test_syn_1m(mode, oracle_mod):
+def test_syn_1m(mode, oracle_mod, layout):
     """syn-1M: full-size parity against the oracle, 2 successive calls."""
     from shud_rhs import synth
     m = synth.synth_model(1_000_000)
     m.step = workload.random_step_inputs(m)
     y = workload.random_state(m)
-    _compare_sequence(m, [y], mode, oracle_mod, ncalls=2, diag=False, label="syn-1M")
+    _compare_sequence(m, [y], mode, oracle_mod, ncalls=2, diag=False, label="syn-1M", layout=layout)
+
+
+def test_fu_nonunit_and_packed_flags(oracle_mod):
+    """fu_Surf / fu_Sub != 1 (cryosphere on) switches the packed kernel to reading them; back to 1 -> skip."""
+    rt = _runtime()
+    m, y0 = cases.ccw()
+    g, o = rt.RhsHandle(m), oracle_mod.OracleRhs(m, 0)
+    g.set_step_inputs(); o.set_step_inputs()
+    rng = np.random.default_rng(4)
+    for fu in [rng.uniform(0.2, 1.0, m.num_ele), np.ones(m.num_ele)]:
+        st = {"fu_surf": fu, "fu_sub": fu[::-1].copy()}
+        g.set_step_inputs(st); o.set_step_inputs(st)
+        for c in range(2):
+            assert_close(g.eval(0.0, y0), o.eval(0.0, y0)[0], what="fu step")

@@ -13,7 +13,9 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("nranks", [2, 4])
 @pytest.mark.parametrize("mode", [0, 1])
-def test_partitioned_handles_bit_identical(nranks, mode):
+@pytest.mark.parametrize("packed", ["1", "0"])
+def test_partitioned_handles_bit_identical(nranks, mode, packed, monkeypatch):
+    monkeypatch.setenv("SHUD_RHS_PACKED", packed)
     from shud_rhs import runtime as rt
     m, y = cases.variant(20000, seed=17)
     single = rt.RhsHandle(m, mode=mode)

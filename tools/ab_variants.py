@@ -1,0 +1,52 @@
+"""A/B the element-kernel build variants on one mesh in one process (interleaved, n rounds).
+Every variant must produce bit-identical ydot (same arithmetic, different schedule/placement).
+usage: python tools/ab_variants.py [--n-ele N] [--variants 0,1,2,...] [--rounds 3] [--reps 20]"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "shud-up_amd"))
+from shud_rhs import runtime, synth, workload  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--n-ele", type=int, default=10_000_000)
+ap.add_argument("--variants", default="soa0,soa3,pk,pk4,pk5",
+                help="soaK = SoA kernel build variant K (SHUD_RHS_PACKED=0, SHUD_RHS_ELE_VARIANT=K); "
+                     "pk / pkW = packed class-layout kernel (min W waves/SIMD)")
+ap.add_argument("--rounds", type=int, default=3)
+ap.add_argument("--reps", type=int, default=20)
+a = ap.parse_args()
+m = synth.synth_model(a.n_ele)
+m.step = workload.random_step_inputs(m)
+y = workload.random_state(m)
+vs = a.variants.split(",")
+
+
+def env_for(v):
+    if v.startswith("soa"):
+        return {"SHUD_RHS_PACKED": "0", "SHUD_RHS_ELE_VARIANT": v[3:] or "0", "SHUD_RHS_PK_WAVES": "0"}
+    return {"SHUD_RHS_PACKED": "1", "SHUD_RHS_ELE_VARIANT": "0", "SHUD_RHS_PK_WAVES": v[2:] or "0"}
+res = {v: [] for v in vs}
+ref = None
+for rnd in range(a.rounds):
+    for v in vs:
+        os.environ.update(env_for(v))
+        h = runtime.RhsHandle(m)
+        h.set_step_inputs()
+        dp, dd = h.device_alloc(8 * m.num_y), h.device_alloc(8 * m.num_y)
+        h.h2d(dp, y)
+        h.eval_device(0.0, dp, dd)
+        out = h.d2h(np.zeros(m.num_y), dd)
+        if ref is None:
+            ref = out
+        same = bool(np.array_equal(out, ref))
+        ms, per = h.time_kernels(0.0, dp, dd, a.reps)
+        res[v].append(per["shud_ele_kernel"])
+        print(f"round {rnd} variant {v:5s} {h.layout()}: ele {per['shud_ele_kernel']:.4f} ms riv {per['shud_riv_kernel']:.4f} "
+              f"ms  bit-identical={same}", flush=True)
+        h.device_free(dp); h.device_free(dd); h.close()
+print(json.dumps({"num_ele": m.num_ele, "ele_ms_median": {v: float(np.median(t)) for v, t in res.items()}}))
