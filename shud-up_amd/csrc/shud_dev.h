@@ -44,23 +44,15 @@ struct DevMesh {
 // parameter tuples once and stores a class id per element, and interleaves the element's own streams
 // into 16-byte records so one lane issues a few wide loads instead of ~45 narrow ones.  Pure layout:
 // every value the kernel computes with is bit-identical to the SoA input.
-struct ClassRec {
-    double macD, macKsatH, vAreaF, KsatH, KsatV, infKsatV, hAreaF, macKsatV;
-    double ThetaS, ThetaR, Beta, infD, Sy, RzD, VegFrac, ImpAF, depression, rough;
-    // per-class subexpressions, evaluated once on the host with the reference's own operation order
-    // (so they are the same doubles the per-element code would produce)
-    double bexp1;    // n / (n - 1.)            satKfun, Equations.cpp:137
-    double bexp2;    // (n - 1.) / n            satKfun, Equations.cpp:137
-    double ths_thr;  // ThetaS - ThetaR         Element.cpp:363, is_sm_et.cpp:133
-    double fc_thr;   // ThetaS * 0.75 - ThetaR  is_sm_et.cpp:133, Element.cpp:314 (ThetaFC - ThetaR)
-    double kmax;     // infKsatV*(1-hAreaF) + macKsatV*hAreaF   Element.cpp:351
-    double omh;      // 1 - hAreaF
-    double hamac;    // hAreaF * macKsatV       Element.cpp:286-288
-    double vb;       // 1 - VegFrac             MD_ET.cpp:345
-    double pj;       // 1 - ImpAF               MD_ET.cpp:346
+// class table, field-major: ctab[field * ncls + class] (one field of every class is contiguous, so a
+// wave-instruction gathering one field for 64 lanes touches a few cache lines, not one per class)
+enum ClassField {
+    CF_macD, CF_macKsatH, CF_vAreaF, CF_KsatH, CF_KsatV, CF_infKsatV, CF_hAreaF, CF_macKsatV, CF_ThetaS,
+    CF_ThetaR, CF_Beta, CF_infD, CF_Sy, CF_RzD, CF_VegFrac, CF_ImpAF, CF_depression, CF_rough, CF_COUNT
 };
 struct DevPacked {
-    const ClassRec *cls;
+    const double *ctab;     // [CF_COUNT][ncls]
+    int ncls;
     const double2 *zz;      // {z_surf, z_bottom}                      (also gathered by neighbours)
     const double2 *aqk;     // {aquifer_depth, bits = class << 32 | flags}  (also gathered by neighbours)
     const int4 *meta;       // {nabr0, nabr1, nabr2, first segment (element-sorted)}

@@ -5,9 +5,10 @@
 // fun_Ele_surface/fun_Ele_sub (MD_ElementFlux.cpp:35-156), fun_Seg_surface/fun_Seg_sub
 // (MD_RiverFlux.cpp:100-126), PassValue's Qe2r sums (MD_f.cpp:228-235) and f_applyDY (MD_f.cpp:65-156).
 // What differs is only how the operands reach the registers:
-//   * every load a lane needs is issued up front and unconditionally (neighbour indices clamped to the
-//     element itself on a boundary edge), so the ~20 independent HBM requests of a wave overlap instead
-//     of queueing behind branches and dependent index loads;
+//   * loads are unconditional (neighbour indices clamped to the element itself on a boundary edge), so
+//     they never queue behind branches; the element's own records are issued up front, each edge's
+//     neighbour data at the top of its (rolled) iteration — at 96 VGPRs five waves per SIMD hide the
+//     latency that three waves holding everything up front could not;
 //   * the element's own streams arrive as 16-byte records (global_load_dwordx4), per-element hydraulic
 //     parameters through a class id into a table that stays in L1/L2;
 //   * single-use streams are loaded/stored non-temporally and workgroups are dealt to XCDs in
@@ -53,7 +54,8 @@ __device__ __forceinline__ double ugw_pk(const DevMesh &m, double ygw_raw, int f
 }
 
 // HOIST: where the neighbour / edge-geometry loads are issued — 0: with the element's own loads at the
-// top (maximum latency cover, most live registers), 1: after the vertical phase, 2: after f_etFlux.
+// top (maximum latency cover, most live registers), 1: after the vertical phase, 2: after f_etFlux,
+// 3: per edge inside a rolled edge loop (fewest live registers; production).
 template <int MODE, bool OPEN, bool DIAG, bool FU1, int LBW = 1, int HOIST = 0>
 __global__ void __launch_bounds__(256, LBW)
 shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int n_compute, int cur,
@@ -91,8 +93,10 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         }
     };
     if (HOIST == 0) load_lateral();
+    (void)nbv;
     const int flags = pk_flags(aqk);
-    const ClassRec *C = &p.cls[pk_class(aqk)];
+    const int cid = pk_class(aqk);
+#define CL(f) p.ctab[CF_##f * p.ncls + cid]
     const int ibc = (int)(int16_t)(flags & 0xffff);
     const int iss = (flags >> 16) & 3;
     const int nseg = (flags >> 18) & 63;
@@ -101,18 +105,19 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     double usf = ysf_raw, uus = yus_raw;
     if (MODE == 1) { usf = (usf >= 0.) ? usf : 0.; uus = (uus >= 0.) ? uus : 0.; }
     const double ugw = ugw_pk<MODE>(m, ygw_raw, flags, i);
-    const double aq = aqk.x, infD = C->infD, ThS = C->ThetaS, ThR = C->ThetaR;
-    const double infK = C->infKsatV;
+    const double aq = aqk.x, infD = CL(infD), ThS = CL(ThetaS), ThR = CL(ThetaR);
+    const double infK = CL(infKsatV), hA = CL(hAreaF), macKV = CL(macKsatV);
     const double fu_surf = fu.x, fu_sub = fu.y;
 
     // ---- f_etFlux (MD_ET.cpp:343-404), serial semantics only ----
     double Es = 0., Eu = 0., Eg = 0., Tu = 0., Tg = 0., eic = csv.y, ibeta = 0.;
     if (MODE == 0) {
         const double satn_prev = csv.x;
-        const double va = C->VegFrac, vb = C->vb, pj = C->pj;
+        const double vf = CL(VegFrac), va = vf, vb = 1. - vf, pj = 1. - CL(ImpAF);
         const double pet = snp.y, ptr = stl.x;
         {
-            double b = (satn_prev * C->ths_thr - ThR) / C->fc_thr;
+            double fc = ThS * K_FC_RATIO;
+            double b = (satn_prev * (ThS - ThR) - ThR) / (fc - ThR);
             b = rmin(rmax(0., b), 1.);
             ibeta = 0.5 * (1 - cos(K_PI * b));
         }
@@ -123,7 +128,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         }
         if (stl.y > K_ZERO) {
             if (eic >= ptr) { Tg = Tu = 0.; eic = ptr * pj * va; }
-            else if (ugw > aq - C->RzD) { Tg = rmin(rmax(0., ugw), (ptr - eic)) * pj * va; Tu = 0.; }
+            else if (ugw > aq - CL(RzD)) { Tg = rmin(rmax(0., ugw), (ptr - eic)) * pj * va; Tu = 0.; }
             else { Tg = 0.; Tu = rmin(rmax(0., uus), ibeta * (ptr - eic)) * pj * va; }
         } else { Tg = Tu = eic = 0.; }
         const double trans = Tg + Tu, evapo = Eu + Eg + Es, eta = eic + evapo + trans;
@@ -141,19 +146,23 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
                     dg.q_eta[i] = eta; dg.i_beta[i] = ibeta; }
     }
 
-    if (HOIST == 2) load_lateral();
+    if (HOIST == 2) {
+        __builtin_amdgcn_sched_barrier(0);
+        load_lateral();
+    }
     // ---- updateElement (Element.cpp:347-384) ----
-    const double ekh = eff_kh(ugw, aq, C->macD, C->macKsatH, C->vAreaF, C->KsatH);
+    const double ekh = eff_kh(ugw, aq, CL(macD), CL(macKsatH), CL(vAreaF), CL(KsatH));
     if (ekh < 0. || ekh > 1e9) report(m.err, 0x02u, 1, i);
     double deficit = aq - ugw;
-    const double kmax = C->kmax;
+    const double kmax = infK * (1. - hA) + macKV * hA;
     double theta, satn, satkr;
     if (deficit <= 0.) { deficit = 0.; satn = 1.; theta = ThS; }
-    else { theta = uus / deficit * ThS; satn = (theta - ThR) / C->ths_thr; }
+    else { theta = uus / deficit * ThS; satn = (theta - ThR) / (ThS - ThR); }
     if (satn > 0.99) { satn = 1.0; satkr = 1.0; theta = ThS; }
     else if (satn <= K_ZERO) { satn = 0.; satkr = 0.; theta = ThR; }
     else {
-        const double tmp = -1. + pow(1. - pow(satn, C->bexp1), C->bexp2);
+        const double n = CL(Beta);
+        const double tmp = -1. + pow(1. - pow(satn, n / (n - 1.)), (n - 1.) / n);
         satkr = sqrt(satn) * tmp * tmp;
     }
     stnt2(&p.cs[cur ^ 1][i], satn, eic);
@@ -167,9 +176,9 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         } else if (av > 0. && deficit > infD) {
             const double grad = 1. + av / infD;
             double ek;
-            if (av > kmax) ek = infK * C->omh + C->hamac * satn;
-            else if (av > infK) ek = satkr * infK * C->omh + C->hamac * satn;
-            else ek = satkr * infK * C->omh;
+            if (av > kmax) ek = infK * (1 - hA) + hA * macKV * satn;
+            else if (av > infK) ek = satkr * infK * (1 - hA) + hA * macKV * satn;
+            else ek = satkr * infK * (1 - hA);
             qi = rmin(av, rmax(0., grad * ek));
         }
     }
@@ -177,11 +186,11 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     // ---- Flux_Recharge (Element.cpp:304-335) ----
     double qr = 0.;
     {
-        const double KV = C->KsatV;
+        const double KV = CL(KsatV);
         if (!(ugw > aq - infD && uus < deficit)) {
             double grad = 0.;
             if (theta > ThR && !(uus <= K_EPSILON)) {
-                grad = (theta - ThR) / C->fc_thr;
+                grad = (theta - ThR) / (ThS * K_FC_RATIO - ThR);
                 grad = rmax(grad, 0.);
             }
             if (!(infK <= 0. || KV <= 0.)) {
@@ -192,9 +201,23 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     }
     const double q_rech = qr * fu_sub;
 
-    if (HOIST == 1) load_lateral();
+    // DY terms that do not depend on the lateral fluxes, in the reference's left-to-right order
+    // (MD_f.cpp:88-90): dsf = ((net_prep - infil) + exfil) - Qsurf/area - Es,  dus complete,
+    // dgw = (recharge - exfil) - Qsub/area - Eg - Tg.  Computing them here ends the live ranges of the
+    // individual ET/vertical terms before the register-heavy lateral loop.
+    const double dsf_head = snp.x - q_infil + q_exfil;
+    const double dgw_head = q_rech - q_exfil;
+    const double sy = CL(Sy);
+    if (i < nown) {
+        const double dus = (q_infil - q_rech - Eu - Tu) / sy;
+        __builtin_nontemporal_store(dus, &dy[nown + i]);
+    }
+    if (HOIST == 1) {
+        __builtin_amdgcn_sched_barrier(0);     // keep the lateral loads (and their registers) out of phase 1
+        load_lateral();
+    }
     // ---- own river segments (fun_Seg_surface / fun_Seg_sub) and Qe2r (PassValue) ----
-    const double zs = zz.x, zb = zz.y, dep = C->depression;
+    const double zs = zz.x, zb = zz.y, dep = CL(depression), rgh = CL(rough);
     double qe2r_surf = 0., qe2r_sub = 0.;
     if (nseg) {
         const double isf_seg = rmax(0., usf - q_infil + q_exfil);
@@ -223,20 +246,39 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     double sumsurf = qe2r_surf, sumsub = qe2r_sub;
     bool nan_q = false;
     const double isf = usf < 0. ? 0. : usf;
-    const double Bv[3] = {e01.x, e01.y, e2a.x};
-    const double Dv[3] = {d01.x, d01.y, d2};
+    if (HOIST == 3) {
+        e01 = ldnt2(&p.ge01[i]);
+        e2a = ldnt2(&p.ge2a[i]);
+        d01 = ldnt2(&p.gd01[i]);
+        d2 = ldnt(&p.gd2[i]);
+    }
 #pragma unroll
-    for (int j = 0; j < 3; j++) {
-        const int nb = nbv[j];
-        const double B = Bv[j];
+    for (int j0 = 0; j0 < 3; j0 += (HOIST == 3 ? 3 : 1)) {
+#pragma unroll 1
+    for (int j = j0; j < (HOIST == 3 ? 3 : j0 + 1); j++) {
+        const int nb = j == 0 ? nbv[0] : j == 1 ? nbv[1] : nbv[2];
+        const double B = j == 0 ? e01.x : j == 1 ? e01.y : e2a.x;
+        const double Dj = j == 0 ? d01.x : j == 1 ? d01.y : d2;
+        double2 nzzj, naqj;
+        double nsfj, ngwj;
+        if (HOIST == 3) {                          // this edge's neighbour data, loaded in the iteration
+            const int ncl = nb >= 0 ? nb : i;
+            nzzj = p.zz[ncl];
+            naqj = p.aqk[ncl];
+            nsfj = Y.sf(ncl);
+            ngwj = Y.gw(ncl);
+        } else {
+            nzzj = nzz[j]; naqj = naq[j]; nsfj = nsf_raw[j]; ngwj = ngw_raw[j];
+        }
         double qsf = 0., qsb = 0.;
         if (nb >= 0) {
-            const ClassRec *Cn = &p.cls[pk_class(naq[j])];
-            double nsf = nsf_raw[j];
+            const int cn = pk_class(naqj);
+#define CN(f) p.ctab[CF_##f * p.ncls + cn]
+            double nsf = nsfj;
             if (MODE == 1) nsf = (nsf >= 0.) ? nsf : 0.;
             nsf = nsf < 0. ? 0. : nsf;
-            const double zsn = nzz[j].x;
-            const double d2n = Dv[j];
+            const double zsn = nzzj.x;
+            const double d2n = Dj;
             const double dh = (isf + zs) - (nsf + zsn);
             double ym = ((isf + zs) > (nsf + zsn)) ? ((isf > dep) ? isf : 0.) : ((nsf > dep) ? nsf : 0.);
             ym = rmin(ym, K_MAXYSURF);
@@ -244,16 +286,17 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
                 const double s = dh / d2n;
                 if (s > 0 && isf <= 0) qsf = 0.;
                 else if (s < 0 && nsf <= 0) qsf = 0.;
-                else qsf = manning(ym * B, 0.5 * (C->rough + Cn->rough), ym, s);   // avgRough, Element.cpp:253
+                else qsf = manning(ym * B, 0.5 * (rgh + CN(rough)), ym, s);   // avgRough, Element.cpp:253
             }
-            const double ugn = ugw_pk<MODE>(m, ngw_raw[j], pk_flags(naq[j]), nb);
-            const double zbn = nzz[j].y;
+            const double ugn = ugw_pk<MODE>(m, ngwj, pk_flags(naqj), nb);
+            const double zbn = nzzj.y;
             const double dhg = (ugw + zb) - (ugn + zbn);
             double q = 0.;
             if (dhg > 0. && ugw <= 0.02) q = 0.;
             else if (dhg < 0. && ugn <= 0.02) q = 0.;
             else {
-                const double ekn = eff_kh(ugn, naq[j].x, Cn->macD, Cn->macKsatH, Cn->vAreaF, Cn->KsatH);
+                const double ekn = eff_kh(ugn, naqj.x, CN(macD), CN(macKsatH), CN(vAreaF), CN(KsatH));
+#undef CN
                 const double ymg = (rmax(ugw, 0.) + rmax(ugn, 0.)) * .5;
                 const double grad = dhg / d2n;
                 const double kmean = 0.5 * (ekh + ekn);
@@ -266,7 +309,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
             const double d2e = m.dist2edge[j * NEl + i];
             if (isf > dep) {
                 const double s = isf / d2e * 0.5;
-                if (s > 0.) qsf = sqrt(s) * cbrt(isf * isf * isf * isf * isf) * B / C->rough;
+                if (s > 0.) qsf = sqrt(s) * cbrt(isf * isf * isf * isf * isf) * B / rgh;
             }
             double q = 0.;
             if (ugw > dep * 10.) {
@@ -280,22 +323,20 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         sumsub += qsb;
         if (DIAG) { dg.qele_surf[j * NEl + i] = qsf; dg.qele_sub[j * NEl + i] = qsb; }
     }
+    }
     if (MODE == 0 && nan_q) report(m.err, 0x01u, 0, i);
 
     // ---- f_applyDY element part (MD_f.cpp:88-131 / MD_f_omp.cpp:26-46) ----
     const double area = e2a.y;
-    double dsf = snp.x - q_infil + q_exfil - sumsurf / area - Es;
-    double dus = q_infil - q_rech - Eu - Tu;
-    double dgw = q_rech - q_exfil - sumsub / area - Eg - Tg;
+    double dsf = dsf_head - sumsurf / area - Es;
+    double dgw = dgw_head - sumsub / area - Eg - Tg;
     if (ibc > 0) dgw = 0;
     else if (ibc < 0) dgw += m.eqbc[-ibc] / area;
     if (iss == 1) dsf += 0.0 / area;
     else if (iss == 2) dgw += 0.0 / area;
-    const double sy = C->Sy;
-    dus /= sy;
+#undef CL
     dgw /= sy;
     __builtin_nontemporal_store(dsf, &dy[i]);
-    __builtin_nontemporal_store(dus, &dy[nown + i]);
     __builtin_nontemporal_store(dgw, &dy[2 * nown + i]);
     if (DIAG) { dg.qele_surf_tot[i] = sumsurf; dg.qele_sub_tot[i] = sumsub; }
 }
@@ -327,10 +368,17 @@ static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, doubl
             case 14: KP(4, 1); return;
             case 20: KP(1, 2); return;
             case 24: KP(4, 2); return;
+            case 30: KP(1, 3); return;
+            case 34: KP(4, 3); return;
+            case 35: KP(5, 3); return;
+            case 36: KP(6, 3); return;
+            case 38: KP(8, 3); return;
             default: break;
         }
     }
-    KP(1, 0);
+    // production build: neighbour data loaded inside a rolled edge loop (HOIST 3) at >= 5 waves/SIMD —
+    // 96 VGPRs, no spills; 0.78 ms vs 0.87 ms for all-loads-up-front at 145 VGPRs / 3 waves (syn-10M A/B)
+    KP(5, 3);
 #undef KP
 }
 

@@ -374,31 +374,20 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     for (int i = 0; i < NE; i++)
         if (seg_off[i + 1] - seg_off[i] > 63) return 0;
     // distinct parameter tuples -> class ids
-    std::vector<ClassRec> table;
+    std::vector<std::vector<double>> table;           // [class][field]
     std::vector<int> cls(NE);
-    struct Key { std::string b; bool operator==(const Key &o) const { return b == o.b; } };
-    struct KH { size_t operator()(const Key &k) const { return std::hash<std::string>()(k.b); } };
-    std::unordered_map<Key, int, KH> ids;
+    std::unordered_map<std::string, int> ids;
     const double dep_default = 0.0002;
+    std::vector<double> r(CF_COUNT);
     for (int i = 0; i < NE; i++) {
-        ClassRec r;
-        r.macD = p->macD[i]; r.macKsatH = p->macKsatH[i]; r.vAreaF = p->geo_vAreaF[i]; r.KsatH = p->KsatH[i];
-        r.KsatV = p->KsatV[i]; r.infKsatV = p->infKsatV[i]; r.hAreaF = p->hAreaF[i]; r.macKsatV = p->macKsatV[i];
-        r.ThetaS = p->ThetaS[i]; r.ThetaR = p->ThetaR[i]; r.Beta = p->Beta[i]; r.infD = p->infD[i]; r.Sy = p->Sy[i];
-        r.RzD = p->RzD[i]; r.VegFrac = p->VegFrac[i]; r.ImpAF = p->ImpAF[i];
-        r.depression = m->depression ? m->depression[i] : dep_default;
-        r.rough = m->rough[i];
-        const double n = r.Beta;
-        r.bexp1 = n / (n - 1.);
-        r.bexp2 = (n - 1.) / n;
-        r.ths_thr = r.ThetaS - r.ThetaR;
-        r.fc_thr = r.ThetaS * 0.75 - r.ThetaR;
-        r.kmax = r.infKsatV * (1. - r.hAreaF) + r.macKsatV * r.hAreaF;
-        r.omh = 1 - r.hAreaF;
-        r.hamac = r.hAreaF * r.macKsatV;
-        r.vb = 1. - r.VegFrac;
-        r.pj = 1. - r.ImpAF;
-        Key k{std::string((const char *)&r, sizeof(r))};
+        r[CF_macD] = p->macD[i]; r[CF_macKsatH] = p->macKsatH[i]; r[CF_vAreaF] = p->geo_vAreaF[i];
+        r[CF_KsatH] = p->KsatH[i]; r[CF_KsatV] = p->KsatV[i]; r[CF_infKsatV] = p->infKsatV[i];
+        r[CF_hAreaF] = p->hAreaF[i]; r[CF_macKsatV] = p->macKsatV[i]; r[CF_ThetaS] = p->ThetaS[i];
+        r[CF_ThetaR] = p->ThetaR[i]; r[CF_Beta] = p->Beta[i]; r[CF_infD] = p->infD[i]; r[CF_Sy] = p->Sy[i];
+        r[CF_RzD] = p->RzD[i]; r[CF_VegFrac] = p->VegFrac[i]; r[CF_ImpAF] = p->ImpAF[i];
+        r[CF_depression] = m->depression ? m->depression[i] : dep_default;
+        r[CF_rough] = m->rough[i];
+        std::string k((const char *)r.data(), r.size() * sizeof(double));
         auto it = ids.find(k);
         if (it == ids.end()) {
             if ((int)table.size() >= (1 << 20)) return 0;
@@ -407,6 +396,10 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         }
         cls[i] = it->second;
     }
+    const int ncls = (int)table.size();
+    std::vector<double> ctab((size_t)CF_COUNT * ncls);
+    for (int c = 0; c < ncls; c++)
+        for (int f = 0; f < CF_COUNT; f++) ctab[(size_t)f * ncls + c] = table[c][f];
     std::vector<double2> zz(NE), aqk(NE), e01(NE), e2a(NE), d01(NE);
     std::vector<double> d2(NE);
     std::vector<int4> meta(NE);
@@ -426,8 +419,8 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     }
     int rc;
     DevPacked &P = h->dp;
-    ClassRec *cls_d; double2 *zz_d, *aqk_d, *e01_d, *e2a_d, *d01_d; double *d2_d; int4 *meta_d;
-    if ((rc = h->upload(&cls_d, table.data(), table.size()))) return rc;
+    double *ctab_d; double2 *zz_d, *aqk_d, *e01_d, *e2a_d, *d01_d; double *d2_d; int4 *meta_d;
+    if ((rc = h->upload(&ctab_d, ctab.data(), ctab.size()))) return rc;
     if ((rc = h->upload(&zz_d, zz.data(), NE))) return rc;
     if ((rc = h->upload(&aqk_d, aqk.data(), NE))) return rc;
     if ((rc = h->upload(&meta_d, meta.data(), NE))) return rc;
@@ -435,7 +428,7 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     if ((rc = h->upload(&e2a_d, e2a.data(), NE))) return rc;
     if ((rc = h->upload(&d01_d, d01.data(), NE))) return rc;
     if ((rc = h->upload(&d2_d, d2.data(), NE))) return rc;
-    P.cls = cls_d; P.zz = zz_d; P.aqk = aqk_d; P.meta = meta_d; P.ge01 = e01_d; P.ge2a = e2a_d; P.gd01 = d01_d;
+    P.ctab = ctab_d; P.ncls = ncls; P.zz = zz_d; P.aqk = aqk_d; P.meta = meta_d; P.ge01 = e01_d; P.ge2a = e2a_d; P.gd01 = d01_d;
     P.gd2 = d2_d;
     if ((rc = h->upload(&P.s_np, (const double2 *)nullptr, NE))) return rc;
     if ((rc = h->upload(&P.s_tl, (const double2 *)nullptr, NE))) return rc;
@@ -443,7 +436,7 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     if ((rc = h->upload(&P.cs[1], (const double2 *)nullptr, NE))) return rc;
     std::vector<double2> ones(NE, make_double2(1.0, 1.0));
     if ((rc = h->upload(&P.s_fu, ones.data(), NE))) return rc;
-    h->n_classes = (int)table.size();
+    h->n_classes = ncls;
     h->packed = true;
     return 0;
 }
