@@ -53,19 +53,28 @@ enum ClassField {
 struct DevPacked {
     const double *ctab;     // [CF_COUNT][ncls]
     int ncls;
-    const double2 *zz;      // {z_surf, z_bottom}                      (also gathered by neighbours)
-    const double2 *aqk;     // {aquifer_depth, bits = class << 32 | flags}  (also gathered by neighbours)
-    const int4 *meta;       // {nabr0, nabr1, nabr2, first segment (element-sorted)}
-    const double2 *ge01;    // {edge0, edge1}
-    const double2 *ge2a;    // {edge2, area}
-    const double2 *gd01;    // {dist2nabor0, dist2nabor1}
-    const double *gd2;      // dist2nabor2
+    const double2 *zz;      // {z_surf, z_bottom}  (aquifer_depth == z_surf - z_bottom, checked at create)
+    const int4 *meta;       // {nabr0, nabr1, nabr2, cf}: cf bits 0-7 iBC (int8), 8-9 iSS class,
+                            //   10-15 #river segments, 16-31 class id  (zz and meta.w are neighbour-gathered)
+    const double2 *ged;     // [3][NE] edge-major {edge_j, dist2nabor_j}
+    const double *area;
+    const int *seg_first;   // first element-sorted segment of each element
+    const double2 *sg_lc;   // [NS] element-sorted segments: {length, Cwr}
+    const double2 *sg_dk;   //   its reach's {depth, KsatH}
+    const int2 *sg_rb;      //   {reach, reach BC column}
+    const double *sg_bt;    //   its reach's BedThick
     double2 *s_np;          // {net_prep, pot_evap}        step inputs (packed by shud_pack_step_kernel)
     double2 *s_tl;          // {pot_tran, lai}
     double2 *s_fu;          // {fu_surf, fu_sub}            read only when not all ones
     double2 *cs[2];         // carried {u_satn, qEleE_IC}, ping-pong
+    // reaches (owned first): 16-byte records
+    const double2 *rv_a;    // {BottomWidth, bankslope}
+    const double2 *rv_b;    // {Length, BedSlope}
+    const double2 *rv_c;    // {Dist2DownStream, avgRough}
+    const double2 *rv_d;    // {depth, 0}
+    const int4 *rv_i;       // {down, BC, first reach-sorted segment, #segments}
+    const int4 *rv_u;       // {up0, up1, up2, #up} (ascending global order); #up = -1: use up_off/up_idx
 };
-// packed flags word: bits 0-15 iBC (int16), 16-17 iSS class, 18-23 number of river segments
 
 struct DevDiag {                     // optional diagnostic outputs (ShudFluxOut), local numbering
     double *qele_surf, *qele_sub, *qele_surf_tot, *qele_sub_tot, *q_infil, *q_exfil, *q_recharge;
@@ -91,7 +100,9 @@ void launch_element_kernel(const DevMesh &m, const YView &Y, double *dy, int n_c
                            int mode, bool open, bool diag, const DevDiag &dg, hipStream_t s, int variant = 0);
 void launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int n_compute,
                                   int cur, int mode, bool open, bool diag, bool fu_unit, const DevDiag &dg,
-                                  hipStream_t s, int pk_waves = 0);
+                                  hipStream_t s);
+void launch_river_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int mode,
+                                bool diag, const DevDiag &dg, hipStream_t s);
 void launch_pack_step_kernel(const DevMesh &m, const DevPacked &p, int n, int cur, unsigned what, hipStream_t s);
 void launch_river_kernel(const DevMesh &m, const YView &Y, double *dy, int mode, bool diag,
                          const DevDiag &dg, hipStream_t s);

@@ -7,8 +7,9 @@
 // What differs is only how the operands reach the registers:
 //   * loads are unconditional (neighbour indices clamped to the element itself on a boundary edge), so
 //     they never queue behind branches; the element's own records are issued up front, each edge's
-//     neighbour data at the top of its (rolled) iteration — at 96 VGPRs five waves per SIMD hide the
+//     neighbour data at the top of its (rolled) iteration — at <= 96 VGPRs five waves per SIMD hide the
 //     latency that three waves holding everything up front could not;
+//   * errors/warnings are aggregated per wave (one atomic per wave, shud_physics.h report_w);
 //   * the element's own streams arrive as 16-byte records (global_load_dwordx4), per-element hydraulic
 //     parameters through a class id into a table that stays in L1/L2;
 //   * single-use streams are loaded/stored non-temporally and workgroups are dealt to XCDs in
@@ -41,75 +42,91 @@ __device__ __forceinline__ void stnt2(double2 *p, double a, double b) {
     __builtin_nontemporal_store(v, (v2d *)p);
 }
 
-__device__ __forceinline__ int pk_flags(double2 a) { return (int)(unsigned)(__double_as_longlong(a.y) & 0xffffffffLL); }
-__device__ __forceinline__ int pk_class(double2 a) { return (int)((unsigned long long)__double_as_longlong(a.y) >> 32); }
+// packed cf word (DevPacked::meta.w)
+__device__ __forceinline__ int cf_ibc(int cf) { return (int)(int8_t)(cf & 0xff); }
+__device__ __forceinline__ int cf_iss(int cf) { return (cf >> 8) & 3; }
+__device__ __forceinline__ int cf_nseg(int cf) { return (cf >> 10) & 63; }
+__device__ __forceinline__ int cf_class(int cf) { return (int)((unsigned)cf >> 16); }
 
-// uYgw of element j from its packed flags (MD_update.cpp:114-125 / MD_f_omp.cpp:119-128)
+// uYgw of element j (MD_update.cpp:114-125 / MD_f_omp.cpp:119-128)
 template <int MODE>
-__device__ __forceinline__ double ugw_pk(const DevMesh &m, double ygw_raw, int flags, int j) {
-    const int ibc = (int)(int16_t)(flags & 0xffff);
+__device__ __forceinline__ double ugw_pk(const DevMesh &m, double ygw_raw, int ibc, int j) {
     if (ibc == 0) return MODE == 0 ? ygw_raw : rmax(0.0, ygw_raw);
     if (ibc > 0) return m.eybc[ibc];
     return m.ugw_stale[j];
 }
 
-// HOIST: where the neighbour / edge-geometry loads are issued — 0: with the element's own loads at the
-// top (maximum latency cover, most live registers), 1: after the vertical phase, 2: after f_etFlux,
-// 3: per edge inside a rolled edge loop (fewest live registers; production).
-template <int MODE, bool OPEN, bool DIAG, bool FU1, int LBW = 1, int HOIST = 0>
-__global__ void __launch_bounds__(256, LBW)
+// class table staged in LDS (record-major [class][field], 144 B per class) when it has <= LDS_CLS_MAX classes:
+// the 18 + 3x5 class lookups per element become LDS reads with immediate offsets instead of dependent L2 trips
+#ifndef SHUD_LDS_CLS_MAX
+#define SHUD_LDS_CLS_MAX 128
+#endif
+constexpr int LDS_CLS_MAX = SHUD_LDS_CLS_MAX;
+
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT>
+__global__ void __launch_bounds__(256, 5)
 shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int n_compute, int cur,
                        DevDiag dg) {
+    __shared__ double lct[LCT ? CF_COUNT * (LDS_CLS_MAX > 0 ? LDS_CLS_MAX : 1) : 1];
+    const int ncls = p.ncls;
+    if (LCT) {
+        for (int t = threadIdx.x; t < ncls * CF_COUNT; t += blockDim.x) {
+            const int c = t / CF_COUNT, f = t - c * CF_COUNT;
+            lct[t] = p.ctab[f * ncls + c];
+        }
+        __syncthreads();
+    }
     const int i = block_id<1>() * blockDim.x + threadIdx.x;
     if (i >= n_compute) return;
     const int NEl = m.num_ele;
     const int nown = Y.n_own;
 
-    // ---------------- issue every load first ----------------
+    // ---------------- state and static records first: saturation (and its two pow calls, the
+    // register peak) is computed while little else is live; ET's inputs are loaded after it ----------------
+    const int4 mt = p.meta[i];
     const double2 zz = p.zz[i];
-    const double2 aqk = p.aqk[i];
-    const int4 mt = ldnt4(&p.meta[i]);
+    const double ysf_raw = Y.sf(i), yus_raw = Y.us(i), ygw_raw = Y.gw(i);
+    const int cf = mt.w;
+    const int cid = cf_class(cf), ibc = cf_ibc(cf);
+#define CL(f) (LCT ? lct[cid * CF_COUNT + CF_##f] : p.ctab[CF_##f * ncls + cid])
+
+    // ---- f_update ----
+    double usf = ysf_raw, uus = yus_raw;
+    if (MODE == 1) { usf = (usf >= 0.) ? usf : 0.; uus = (uus >= 0.) ? uus : 0.; }
+    const double ugw = ugw_pk<MODE>(m, ygw_raw, ibc, i);
+    const double zs = zz.x, zb = zz.y;
+    const double aq = zs - zb;                    // InitElement after rmSinks (Model_Data.cpp:262-264)
+
+    // ---- updateElement (Element.cpp:347-384); pure function of the state, hoisted above f_etFlux ----
+    const double ekh = eff_kh(ugw, aq, CL(macD), CL(macKsatH), CL(vAreaF), CL(KsatH));
+    report_w(m.err, ekh < 0. || ekh > 1e9, 0x02u, 1, i);
+    double deficit = aq - ugw;
+    double theta, satn, satkr;
+    {
+        const double ThS = CL(ThetaS), ThR = CL(ThetaR);
+        if (deficit <= 0.) { deficit = 0.; satn = 1.; theta = ThS; }
+        else { theta = SDIV(uus, deficit) * ThS; satn = SDIV(theta - ThR, ThS - ThR); }
+        if (satn > 0.99) { satn = 1.0; satkr = 1.0; theta = ThS; }
+        else if (satn <= K_ZERO) { satn = 0.; satkr = 0.; theta = ThR; }
+        else {   // satKfun, Equations.cpp:136-141
+            const double n = CL(Beta);
+            const double tmp = -1. + SPOW(1. - SPOW(satn, SDIV(n, n - 1.)), SDIV(n - 1., n));
+            satkr = SSQRT(satn) * tmp * tmp;
+        }
+    }
+
     const double2 snp = ldnt2(&p.s_np[i]), stl = ldnt2(&p.s_tl[i]);
     const double etp = ldnt(&m.etp[i]);
     double2 fu;
     if (FU1) { fu.x = 1.0; fu.y = 1.0; } else fu = ldnt2(&p.s_fu[i]);
     const double2 csv = ldnt2(&p.cs[cur][i]);
-    const double ysf_raw = Y.sf(i), yus_raw = Y.us(i), ygw_raw = Y.gw(i);
-    int nbv[3] = {mt.x, mt.y, mt.z};
-    double2 nzz[3], naq[3], e01, e2a, d01;
-    double nsf_raw[3], ngw_raw[3], d2;
-    auto load_lateral = [&]() {
-        e01 = ldnt2(&p.ge01[i]);
-        e2a = ldnt2(&p.ge2a[i]);
-        d01 = ldnt2(&p.gd01[i]);
-        d2 = ldnt(&p.gd2[i]);
-#pragma unroll
-        for (int j = 0; j < 3; j++) {
-            const int nc = nbv[j] >= 0 ? nbv[j] : i;     // boundary edge: a harmless in-bounds load
-            nzz[j] = p.zz[nc];
-            naq[j] = p.aqk[nc];
-            nsf_raw[j] = Y.sf(nc);
-            ngw_raw[j] = Y.gw(nc);
-        }
-    };
-    if (HOIST == 0) load_lateral();
-    (void)nbv;
-    const int flags = pk_flags(aqk);
-    const int cid = pk_class(aqk);
-#define CL(f) p.ctab[CF_##f * p.ncls + cid]
-    const int ibc = (int)(int16_t)(flags & 0xffff);
-    const int iss = (flags >> 16) & 3;
-    const int nseg = (flags >> 18) & 63;
-
-    // ---- f_update ----
-    double usf = ysf_raw, uus = yus_raw;
-    if (MODE == 1) { usf = (usf >= 0.) ? usf : 0.; uus = (uus >= 0.) ? uus : 0.; }
-    const double ugw = ugw_pk<MODE>(m, ygw_raw, flags, i);
-    const double aq = aqk.x, infD = CL(infD), ThS = CL(ThetaS), ThR = CL(ThetaR);
+    const int sfirst = p.seg_first[i];
+    const int iss = cf_iss(cf), nseg = cf_nseg(cf);
+    const double infD = CL(infD), ThS = CL(ThetaS), ThR = CL(ThetaR);
     const double infK = CL(infKsatV), hA = CL(hAreaF), macKV = CL(macKsatV);
     const double fu_surf = fu.x, fu_sub = fu.y;
 
-    // ---- f_etFlux (MD_ET.cpp:343-404), serial semantics only ----
+    // ---- f_etFlux (MD_ET.cpp:343-404), serial semantics only (reads the previous call's u_satn) ----
     double Es = 0., Eu = 0., Eg = 0., Tu = 0., Tg = 0., eic = csv.y, ibeta = 0.;
     if (MODE == 0) {
         const double satn_prev = csv.x;
@@ -117,9 +134,9 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         const double pet = snp.y, ptr = stl.x;
         {
             double fc = ThS * K_FC_RATIO;
-            double b = (satn_prev * (ThS - ThR) - ThR) / (fc - ThR);
+            double b = SDIV(satn_prev * (ThS - ThR) - ThR, fc - ThR);
             b = rmin(rmax(0., b), 1.);
-            ibeta = 0.5 * (1 - cos(K_PI * b));
+            ibeta = 0.5 * (1 - SCOS(K_PI * b));
         }
         Es = rmin(rmax(0., usf), pet) * vb;
         if (Es < pet) {
@@ -132,49 +149,30 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
             else { Tg = 0.; Tu = rmin(rmax(0., uus), ibeta * (ptr - eic)) * pj * va; }
         } else { Tg = Tu = eic = 0.; }
         const double trans = Tg + Tu, evapo = Eu + Eg + Es, eta = eic + evapo + trans;
-        if (eta > etp * 2.) { atomicAdd(&m.err->n_warn, 1ULL); report(m.err, 0x10u, 4, i); }
-        bool neg = false;
+        report_w(m.err, eta > etp * 2., 0x10u, 4, i, true);      // printf warning, MD_ET.cpp:391-393
+        bool neg = false;                                         // CheckNonNegative, functions.cpp:148-154
         neg |= (Es < 0.0 || isnan(Es) || isinf(Es) || fabs(Es - K_NA_VALUE) < K_ZERO);
         neg |= (Eu < 0.0 || isnan(Eu) || isinf(Eu) || fabs(Eu - K_NA_VALUE) < K_ZERO);
         neg |= (Eg < 0.0 || isnan(Eg) || isinf(Eg) || fabs(Eg - K_NA_VALUE) < K_ZERO);
         neg |= (Tu < 0.0 || isnan(Tu) || isinf(Tu) || fabs(Tu - K_NA_VALUE) < K_ZERO);
         neg |= (Tg < 0.0 || isnan(Tg) || isinf(Tg) || fabs(Tg - K_NA_VALUE) < K_ZERO);
-        if (neg) report(m.err, 0x04u, 2, i);
-        else if (isnan(eta) || isinf(eta) || isnan(evapo) || isinf(evapo) || isnan(trans) || isinf(trans))
-            report(m.err, 0x08u, 3, i);
+        report_w(m.err, neg, 0x04u, 2, i);
+        report_w(m.err, !neg && (isnan(eta) || isinf(eta) || isnan(evapo) || isinf(evapo) || isnan(trans) ||
+                                 isinf(trans)), 0x08u, 3, i);
         if (DIAG) { dg.q_es[i] = Es; dg.q_eu[i] = Eu; dg.q_eg[i] = Eg; dg.q_tu[i] = Tu; dg.q_tg[i] = Tg;
                     dg.q_eta[i] = eta; dg.i_beta[i] = ibeta; }
     }
-
-    if (HOIST == 2) {
-        __builtin_amdgcn_sched_barrier(0);
-        load_lateral();
-    }
-    // ---- updateElement (Element.cpp:347-384) ----
-    const double ekh = eff_kh(ugw, aq, CL(macD), CL(macKsatH), CL(vAreaF), CL(KsatH));
-    if (ekh < 0. || ekh > 1e9) report(m.err, 0x02u, 1, i);
-    double deficit = aq - ugw;
-    const double kmax = infK * (1. - hA) + macKV * hA;
-    double theta, satn, satkr;
-    if (deficit <= 0.) { deficit = 0.; satn = 1.; theta = ThS; }
-    else { theta = uus / deficit * ThS; satn = (theta - ThR) / (ThS - ThR); }
-    if (satn > 0.99) { satn = 1.0; satkr = 1.0; theta = ThS; }
-    else if (satn <= K_ZERO) { satn = 0.; satkr = 0.; theta = ThR; }
-    else {
-        const double n = CL(Beta);
-        const double tmp = -1. + pow(1. - pow(satn, n / (n - 1.)), (n - 1.) / n);
-        satkr = sqrt(satn) * tmp * tmp;
-    }
     stnt2(&p.cs[cur ^ 1][i], satn, eic);
+    const double kmax = infK * (1. - hA) + macKV * hA;
 
     // ---- Flux_Infiltration (Element.cpp:271-303) ----
     double qi = 0., qex = 0.;
     {
         const double av = usf + snp.x;
         if (ugw + uus > aq || deficit < uus) {
-            qex = fabs(ugw + uus - aq) / aq * kmax;
+            qex = SDIV(fabs(ugw + uus - aq), aq) * kmax;
         } else if (av > 0. && deficit > infD) {
-            const double grad = 1. + av / infD;
+            const double grad = 1. + SDIV(av, infD);
             double ek;
             if (av > kmax) ek = infK * (1 - hA) + hA * macKV * satn;
             else if (av > infK) ek = satkr * infK * (1 - hA) + hA * macKV * satn;
@@ -183,19 +181,19 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         }
     }
     const double q_infil = qi * fu_surf, q_exfil = qex * fu_surf;
-    // ---- Flux_Recharge (Element.cpp:304-335) ----
+    // ---- Flux_Recharge (Element.cpp:304-335), meanHarmonic (Equations.hpp:45-48) ----
     double qr = 0.;
     {
         const double KV = CL(KsatV);
         if (!(ugw > aq - infD && uus < deficit)) {
             double grad = 0.;
             if (theta > ThR && !(uus <= K_EPSILON)) {
-                grad = (theta - ThR) / (ThS * K_FC_RATIO - ThR);
+                grad = SDIV(theta - ThR, ThS * K_FC_RATIO - ThR);
                 grad = rmax(grad, 0.);
             }
             if (!(infK <= 0. || KV <= 0.)) {
                 const double ku = infK * satkr;
-                qr = grad * ((ku * KV) * (deficit + ugw) / (deficit * KV + ugw * ku));
+                qr = grad * SDIV((ku * KV) * (deficit + ugw), deficit * KV + ugw * ku);
             }
         }
     }
@@ -203,33 +201,28 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
 
     // DY terms that do not depend on the lateral fluxes, in the reference's left-to-right order
     // (MD_f.cpp:88-90): dsf = ((net_prep - infil) + exfil) - Qsurf/area - Es,  dus complete,
-    // dgw = (recharge - exfil) - Qsub/area - Eg - Tg.  Computing them here ends the live ranges of the
-    // individual ET/vertical terms before the register-heavy lateral loop.
+    // dgw = (recharge - exfil) - Qsub/area - Eg - Tg.  Ends the ET/vertical live ranges early.
     const double dsf_head = snp.x - q_infil + q_exfil;
     const double dgw_head = q_rech - q_exfil;
-    const double sy = CL(Sy);
-    if (i < nown) {
-        const double dus = (q_infil - q_rech - Eu - Tu) / sy;
-        __builtin_nontemporal_store(dus, &dy[nown + i]);
-    }
-    if (HOIST == 1) {
-        __builtin_amdgcn_sched_barrier(0);     // keep the lateral loads (and their registers) out of phase 1
-        load_lateral();
-    }
+    if (i < nown) __builtin_nontemporal_store(SDIV(q_infil - q_rech - Eu - Tu, CL(Sy)), &dy[nown + i]);
+
     // ---- own river segments (fun_Seg_surface / fun_Seg_sub) and Qe2r (PassValue) ----
-    const double zs = zz.x, zb = zz.y, dep = CL(depression), rgh = CL(rough);
+    const double dep = CL(depression), rgh = CL(rough);
     double qe2r_surf = 0., qe2r_sub = 0.;
     if (nseg) {
         const double isf_seg = rmax(0., usf - q_infil + q_exfil);
-        for (int k = mt.w, k1 = mt.w + nseg; k < k1; k++) {
-            const int r = m.seg_riv[k];
-            double yraw;
-            const double yr = uriv_of<MODE>(m, Y, r, &yraw);
-            const double rdep = m.riv_depth[r];
-            const double L = m.seg_len[k];
-            const double qs = weir_jtoi(zs, isf_seg, zs - rdep, yr, zs + 0.0, m.seg_cwr[k], L, dep);
-            const double qg = r2e_gw(yr, zs - rdep, ugw, zb, ekh, m.riv_ksath[r], L, m.riv_bedthick[r]) * fu_sub;
-            m.qseg_surf[k] = qs;
+        for (int k = sfirst, k1 = k + nseg; k < k1; k++) {
+            // one 48-B element-sorted record per segment: its own fields plus its reach's statics
+            const double2 lc = p.sg_lc[k], dk = p.sg_dk[k];
+            const int2 rb = p.sg_rb[k];
+            const double bt = p.sg_bt[k];
+            double yr = Y.riv(rb.x);                      // uriv_of (shud_physics.h), BC from the record
+            if (MODE == 1) yr = (yr >= 0.) ? yr : 0.;
+            if (rb.y > 0) yr = m.rybc[rb.y];
+            const double rdep = dk.x, L = lc.x;
+            const double qs = weir_jtoi(zs, isf_seg, zs - rdep, yr, zs + 0.0, lc.y, L, dep);
+            const double qg = r2e_gw(yr, zs - rdep, ugw, zb, ekh, dk.y, L, bt) * fu_sub;
+            m.qseg_surf[k] = qs;           // element-sorted: consecutive lanes write consecutive k
             m.qseg_sub[k] = qg;
             qe2r_surf += -qs;
             qe2r_sub += -qg;
@@ -242,69 +235,55 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     }
     if (i >= nown) return;    // ghost element of a partition: vertical + segments only
 
-    // ---- fun_Ele_surface / fun_Ele_sub over 3 edges (MD_ElementFlux.cpp:35-156) ----
-    double sumsurf = qe2r_surf, sumsub = qe2r_sub;
+    // ---- fun_Ele_surface / fun_Ele_sub, one edge per (rolled) iteration (MD_ElementFlux.cpp:35-156) ----
+    // each edge's neighbour data is loaded at the top of its iteration; keeping the loop rolled holds the
+    // kernel at 96 VGPRs = 5 waves/SIMD (all three edges in flight at once needs ~145 = 3 waves: slower)
+    double sumsurf = qe2r_surf, sumsub = qe2r_sub;     // QeleSurfTot = Qe2r + sum_j QeleSurf[j]
     bool nan_q = false;
     const double isf = usf < 0. ? 0. : usf;
-    if (HOIST == 3) {
-        e01 = ldnt2(&p.ge01[i]);
-        e2a = ldnt2(&p.ge2a[i]);
-        d01 = ldnt2(&p.gd01[i]);
-        d2 = ldnt(&p.gd2[i]);
-    }
-#pragma unroll
-    for (int j0 = 0; j0 < 3; j0 += (HOIST == 3 ? 3 : 1)) {
 #pragma unroll 1
-    for (int j = j0; j < (HOIST == 3 ? 3 : j0 + 1); j++) {
-        const int nb = j == 0 ? nbv[0] : j == 1 ? nbv[1] : nbv[2];
-        const double B = j == 0 ? e01.x : j == 1 ? e01.y : e2a.x;
-        const double Dj = j == 0 ? d01.x : j == 1 ? d01.y : d2;
-        double2 nzzj, naqj;
-        double nsfj, ngwj;
-        if (HOIST == 3) {                          // this edge's neighbour data, loaded in the iteration
-            const int ncl = nb >= 0 ? nb : i;
-            nzzj = p.zz[ncl];
-            naqj = p.aqk[ncl];
-            nsfj = Y.sf(ncl);
-            ngwj = Y.gw(ncl);
-        } else {
-            nzzj = nzz[j]; naqj = naq[j]; nsfj = nsf_raw[j]; ngwj = ngw_raw[j];
-        }
+    for (int j = 0; j < 3; j++) {
+        const int nb = j == 0 ? mt.x : j == 1 ? mt.y : mt.z;
+        const double2 g = ldnt2(&p.ged[(size_t)j * NEl + i]);
+        const int nc = nb >= 0 ? nb : i;                  // boundary edge: harmless in-bounds loads
+        const double2 nzz = p.zz[nc];
+        const int ncf = p.meta[nc].w;
+        const double nsf_raw = Y.sf(nc), ngw_raw = Y.gw(nc);
+        const double B = g.x, d2n = g.y;
         double qsf = 0., qsb = 0.;
         if (nb >= 0) {
-            const int cn = pk_class(naqj);
-#define CN(f) p.ctab[CF_##f * p.ncls + cn]
-            double nsf = nsfj;
+            const int cn = cf_class(ncf);
+#define CN(f) (LCT ? lct[cn * CF_COUNT + CF_##f] : p.ctab[CF_##f * ncls + cn])
+            double nsf = nsf_raw;
             if (MODE == 1) nsf = (nsf >= 0.) ? nsf : 0.;
             nsf = nsf < 0. ? 0. : nsf;
-            const double zsn = nzzj.x;
-            const double d2n = Dj;
+            const double zsn = nzz.x;
             const double dh = (isf + zs) - (nsf + zsn);
             double ym = ((isf + zs) > (nsf + zsn)) ? ((isf > dep) ? isf : 0.) : ((nsf > dep) ? nsf : 0.);
             ym = rmin(ym, K_MAXYSURF);
             if (ym > 0.) {
-                const double s = dh / d2n;
+                const double s = SDIV(dh, d2n);
                 if (s > 0 && isf <= 0) qsf = 0.;
                 else if (s < 0 && nsf <= 0) qsf = 0.;
                 else qsf = manning(ym * B, 0.5 * (rgh + CN(rough)), ym, s);   // avgRough, Element.cpp:253
             }
-            const double ugn = ugw_pk<MODE>(m, ngwj, pk_flags(naqj), nb);
-            const double zbn = nzzj.y;
+            const double ugn = ugw_pk<MODE>(m, ngw_raw, cf_ibc(ncf), nb);
+            const double zbn = nzz.y;
             const double dhg = (ugw + zb) - (ugn + zbn);
             double q = 0.;
             if (dhg > 0. && ugw <= 0.02) q = 0.;
             else if (dhg < 0. && ugn <= 0.02) q = 0.;
             else {
-                const double ekn = eff_kh(ugn, naqj.x, CN(macD), CN(macKsatH), CN(vAreaF), CN(KsatH));
+                const double ekn = eff_kh(ugn, zsn - zbn, CN(macD), CN(macKsatH), CN(vAreaF), CN(KsatH));
 #undef CN
                 const double ymg = (rmax(ugw, 0.) + rmax(ugn, 0.)) * .5;
-                const double grad = dhg / d2n;
+                const double grad = SDIV(dhg, d2n);
                 const double kmean = 0.5 * (ekh + ekn);
                 q = kmean * grad * ymg * B;
             }
             qsb = q * fu_sub;
         } else if (!OPEN) {
-            qsb = 0. * fu_sub;
+            qsb = 0. * fu_sub;                            // closed boundary: Q = 0, times fu_Sub
         } else {
             const double d2e = m.dist2edge[j * NEl + i];
             if (isf > dep) {
@@ -323,22 +302,162 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         sumsub += qsb;
         if (DIAG) { dg.qele_surf[j * NEl + i] = qsf; dg.qele_sub[j * NEl + i] = qsb; }
     }
-    }
-    if (MODE == 0 && nan_q) report(m.err, 0x01u, 0, i);
+    if (MODE == 0) report_w(m.err, nan_q, 0x01u, 0, i);       // CheckNANij, MD_f.cpp:73-74
 
     // ---- f_applyDY element part (MD_f.cpp:88-131 / MD_f_omp.cpp:26-46) ----
-    const double area = e2a.y;
-    double dsf = dsf_head - sumsurf / area - Es;
-    double dgw = dgw_head - sumsub / area - Eg - Tg;
+    const double area = ldnt(&p.area[i]);
+    double dsf = dsf_head - SDIV(sumsurf, area) - Es;
+    double dgw = dgw_head - SDIV(sumsub, area) - Eg - Tg;
     if (ibc > 0) dgw = 0;
-    else if (ibc < 0) dgw += m.eqbc[-ibc] / area;
-    if (iss == 1) dsf += 0.0 / area;
+    else if (ibc < 0) dgw += SDIV(m.eqbc[-ibc], area);
+    if (iss == 1) dsf += 0.0 / area;                          // QSS is never assigned: 0
     else if (iss == 2) dgw += 0.0 / area;
+    dgw = SDIV(dgw, CL(Sy));
 #undef CL
-    dgw /= sy;
     __builtin_nontemporal_store(dsf, &dy[i]);
     __builtin_nontemporal_store(dgw, &dy[2 * nown + i]);
     if (DIAG) { dg.qele_surf_tot[i] = sumsurf; dg.qele_sub_tot[i] = sumsub; }
+}
+
+// ===================================================================================
+// river kernel on 16-byte reach records (same physics and order as shud_riv_kernel, shud_kernels.hip)
+// ===================================================================================
+struct RivP {
+    double w0, bs, len, slope, d2d, n, depth;
+    int down, bc;
+};
+__device__ __forceinline__ RivP riv_load(const DevPacked &p, int r) {
+    const double2 a = p.rv_a[r], b = p.rv_b[r], c = p.rv_c[r], d = p.rv_d[r];
+    const int4 ii = p.rv_i[r];
+    RivP o;
+    o.w0 = a.x; o.bs = a.y; o.len = b.x; o.slope = b.y; o.d2d = c.x; o.n = c.y; o.depth = d.x;
+    o.down = ii.x; o.bc = ii.y;
+    return o;
+}
+// River.cpp:49-62 updateRiver (pre-BC stage) + River.hpp:115-127
+__device__ __forceinline__ RivGeom riv_geom_p(const RivP &q, double y) {
+    RivGeom g;
+    const double topw = y * q.bs * 2.0 + q.w0;
+    const double a = y * (q.w0 + y * q.bs);
+    const double ys = y * q.bs;
+    const double per = 2.0 * sqrt(y * y + ys * ys) + q.w0;
+    const double eqw = 0.5 * ((y * q.bs * 2.0 + q.w0) + q.w0);
+    const double ta = eqw * q.len;
+    g.topw = (topw < 0.) ? 0. : topw;
+    g.csarea = (a < 0.) ? 0. : a;
+    g.csperem = (per < 0.) ? 0. : per;
+    g.toparea = (ta < 0.) ? 0. : ta;
+    return g;
+}
+// stage after f_update's clamp + BC override; *yg = the value updateRiver() saw
+template <int MODE>
+__device__ __forceinline__ double riv_stage_p(const DevMesh &m, const YView &Y, int r, int bc, double *yg) {
+    double yr = Y.riv(r);
+    if (MODE == 1) yr = (yr >= 0.) ? yr : 0.;
+    *yg = yr;
+    return bc > 0 ? m.rybc[bc] : yr;
+}
+// MD_RiverFlux.cpp:5-63: reach q with stage uq and geometry g; its downstream has stage ud, depth, slope
+__device__ __forceinline__ double riv_down_p(const RivP &q, double uq, const RivGeom &g, double ud, double ddepth,
+                                             double dslope) {
+    if (q.down >= 0) {
+        const double smean = (q.slope + dslope) * 0.5;
+        const double s = ((uq - q.depth) - (ud - ddepth)) / q.d2d + smean;
+        const double R = (g.csperem <= K_ZERO) ? 0. : (g.csarea / g.csperem);
+        return manning(g.csarea, q.n, R, s);
+    } else if (q.down >= -3) {
+        const double s = q.slope + uq * 2. / q.len;
+        const double R = (g.csperem <= 0.) ? 0. : (g.csarea / g.csperem);
+        return manning(g.csarea, q.n, R, s);
+    }
+    return g.csarea * sqrt(K_GRAV * uq) * 60.;
+}
+
+template <int MODE, bool DIAG>
+__global__ void __launch_bounds__(256)
+shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, DevDiag dg) {
+    // XCD-chunked workgroup order: a reach's up/downstream records sit a few blocks away in index space,
+    // so they are L2 hits on the same XCD instead of fabric round trips (speed only)
+    const int r = block_id<1>() * blockDim.x + threadIdx.x;
+    if (r >= Y.n_own_riv) return;
+    const RivP q = riv_load(p, r);
+    const int4 ii = p.rv_i[r];
+    const int4 up = p.rv_u[r];
+    double yg;
+    const double ur = riv_stage_p<MODE>(m, Y, r, q.bc, &yg);
+    const RivGeom g = riv_geom_p(q, yg);
+    double qdown;
+    {
+        const int d = q.down >= 0 ? q.down : r;                 // clamped: unconditional loads
+        const double2 bd = p.rv_b[d], dd = p.rv_d[d];
+        const int bcd = p.rv_i[d].y;
+        double ydg;
+        const double ud = riv_stage_p<MODE>(m, Y, d, bcd, &ydg);
+        qdown = riv_down_p(q, ur, g, ud, dd.x, bd.y);
+    }
+    // junction: QrivUp[down] += -QrivDown[i], i ascending (MD_f.cpp:236-240)
+    double qup = 0.;
+    const int nup = up.w;
+    if (nup >= 0) {
+        const int uv[3] = {up.x, up.y, up.z};
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            if (k < nup) {
+                const int u = uv[k];
+                const RivP qu = riv_load(p, u);
+                double yu;
+                const double uu = riv_stage_p<MODE>(m, Y, u, qu.bc, &yu);
+                qup += -riv_down_p(qu, uu, riv_geom_p(qu, yu), ur, q.depth, q.slope);
+            }
+        }
+    } else {
+        for (int k = m.up_off[r], k1 = m.up_off[r + 1]; k < k1; k++) {
+            const int u = m.up_idx[k];
+            const RivP qu = riv_load(p, u);
+            double yu;
+            const double uu = riv_stage_p<MODE>(m, Y, u, qu.bc, &yu);
+            qup += -riv_down_p(qu, uu, riv_geom_p(qu, yu), ur, q.depth, q.slope);
+        }
+    }
+    // segment sums, ascending reference segment order (MD_f.cpp:228-235), gathered from the element-sorted
+    // fluxes (scattered 8-B writes from the element kernel cost more than these gathers)
+    double qsurf = 0., qsub = 0.;
+    for (int k = ii.z, k1 = ii.z + ii.w; k < k1; k++) {
+        const int ps = m.rseg_pos[k];
+        qsurf += m.qseg_surf[ps];
+        qsub += m.qseg_sub[ps];
+    }
+    const double qbc = (q.bc < 0) ? m.rqbc[-q.bc] : 0.0;
+    double dv;
+    if (q.bc > 0) dv = 0.;
+    else if (MODE == 0) {   // MD_f.cpp:162-166
+        dv = (-qup - qsurf - qsub - qdown + qbc) / q.len;
+        if (dv < -1. * g.csarea) dv = -1. * g.csarea;
+        if (dv == 0.) dv = 0.;                                        // fun_dAtodY functions.hpp:141-153
+        else if (fabs(q.bs) < K_EPS_SLOPE) dv = dv / g.topw;
+        else {                                                        // Quadratic functions.hpp:125-139
+            const double sa = fabs(q.bs);
+            const double cc = g.topw * g.topw + 4 * sa * dv;
+            dv = (cc < K_ZERO) ? -1. * g.topw / (2. * sa) : (-g.topw + sqrt(cc)) / (2 * sa);
+        }
+    } else {                // MD_f_omp.cpp:59
+        dv = (-qup - qsurf - qsub - qdown + qbc) / g.toparea;
+    }
+    dy[3 * Y.n_own + r] = dv;
+    if (DIAG) { dg.qriv_down[r] = qdown; dg.qriv_up[r] = qup; dg.qriv_surf[r] = qsurf; dg.qriv_sub[r] = qsub; }
+}
+
+void launch_river_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int mode,
+                                bool diag, const DevDiag &dg, hipStream_t s) {
+    if (Y.n_own_riv <= 0) return;
+    const dim3 grid(((Y.n_own_riv + 255) / 256 + 7) / 8 * 8), blk(256);
+    if (mode == 0) {
+        if (diag) hipLaunchKernelGGL((shud_riv_kernel_packed<0, true>), grid, blk, 0, s, m, p, Y, dy, dg);
+        else hipLaunchKernelGGL((shud_riv_kernel_packed<0, false>), grid, blk, 0, s, m, p, Y, dy, dg);
+    } else {
+        if (diag) hipLaunchKernelGGL((shud_riv_kernel_packed<1, true>), grid, blk, 0, s, m, p, Y, dy, dg);
+        else hipLaunchKernelGGL((shud_riv_kernel_packed<1, false>), grid, blk, 0, s, m, p, Y, dy, dg);
+    }
 }
 
 // step inputs (SoA staging in DevMesh) -> packed records; `what` bits: 1 np, 2 tl, 4 fu, 8 u_satn, 16 e_ic
@@ -353,40 +472,21 @@ shud_pack_step_kernel(DevMesh m, DevPacked p, int n, int cur, unsigned what) {
     if (what & 16) p.cs[cur][i].y = m.e_ic[0][i];
 }
 
-// pk_waves (SHUD_RHS_PK_WAVES, A/B only): minimum waves per SIMD, 0 = compiler's choice
-template <int MODE, bool OPEN, bool DIAG, bool FU1>
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT>
 static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int n, int cur,
-                     const DevDiag &dg, hipStream_t s, int pk_waves) {
+                     const DevDiag &dg, hipStream_t s) {
     int nb = (n + 255) / 256;
     nb = (nb + 7) / 8 * 8;                  // block_id<1> deals blocks to XCDs in contiguous chunks
-#define KP(W, H) hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, W, H>), dim3(nb), dim3(256), 0, s, \
-                                    m, p, Y, dy, n, cur, dg)
-    if (MODE == 0 && !OPEN && !DIAG) {       // A/B builds: pk_waves = W + 10 * HOIST
-        switch (pk_waves) {
-            case 4: KP(4, 0); return;
-            case 10: KP(1, 1); return;
-            case 14: KP(4, 1); return;
-            case 20: KP(1, 2); return;
-            case 24: KP(4, 2); return;
-            case 30: KP(1, 3); return;
-            case 34: KP(4, 3); return;
-            case 35: KP(5, 3); return;
-            case 36: KP(6, 3); return;
-            case 38: KP(8, 3); return;
-            default: break;
-        }
-    }
-    // production build: neighbour data loaded inside a rolled edge loop (HOIST 3) at >= 5 waves/SIMD —
-    // 96 VGPRs, no spills; 0.78 ms vs 0.87 ms for all-loads-up-front at 145 VGPRs / 3 waves (syn-10M A/B)
-    KP(5, 3);
-#undef KP
+    hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT>), dim3(nb), dim3(256), 0, s, m, p, Y, dy, n,
+                       cur, dg);
 }
 
 void launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int n_compute,
                                   int cur, int mode, bool open, bool diag, bool fu_unit, const DevDiag &dg,
-                                  hipStream_t s, int pk_waves) {
+                                  hipStream_t s) {
     if (n_compute <= 0) return;
-#define LP(MO, OP, DI, FU) launch_p<MO, OP, DI, FU>(m, p, Y, dy, n_compute, cur, dg, s, pk_waves)
+#define LP(MO, OP, DI, FU) do { if (p.ncls <= LDS_CLS_MAX) launch_p<MO, OP, DI, FU, true>(m, p, Y, dy, n_compute, cur, dg, s); \
+                                 else launch_p<MO, OP, DI, FU, false>(m, p, Y, dy, n_compute, cur, dg, s); } while (0)
 #define LFU(MO, OP, DI) do { if (fu_unit) LP(MO, OP, DI, true); else LP(MO, OP, DI, false); } while (0)
 #define LDI(MO, OP) do { if (diag) LFU(MO, OP, true); else LFU(MO, OP, false); } while (0)
 #define LOP(MO) do { if (open) LDI(MO, true); else LDI(MO, false); } while (0)

@@ -69,16 +69,16 @@ shud_ele_kernel(DevMesh m, YView Y, double *__restrict__ dy, int n_compute, int 
             else { Tg = 0.; Tu = rmin(rmax(0., uus), ibeta * (ptr - eic)) * pj * va; }
         } else { Tg = Tu = eic = 0.; }
         const double trans = Tg + Tu, evapo = Eu + Eg + Es, eta = eic + evapo + trans;
-        if (eta > ld1<VAR>(&m.etp[i]) * 2.) { atomicAdd(&m.err->n_warn, 1ULL); report(m.err, 0x10u, 4, i); }
+        report_w(m.err, eta > ld1<VAR>(&m.etp[i]) * 2., 0x10u, 4, i, true);
         bool neg = false;
         neg |= (Es < 0.0 || isnan(Es) || isinf(Es) || fabs(Es - K_NA_VALUE) < K_ZERO);
         neg |= (Eu < 0.0 || isnan(Eu) || isinf(Eu) || fabs(Eu - K_NA_VALUE) < K_ZERO);
         neg |= (Eg < 0.0 || isnan(Eg) || isinf(Eg) || fabs(Eg - K_NA_VALUE) < K_ZERO);
         neg |= (Tu < 0.0 || isnan(Tu) || isinf(Tu) || fabs(Tu - K_NA_VALUE) < K_ZERO);
         neg |= (Tg < 0.0 || isnan(Tg) || isinf(Tg) || fabs(Tg - K_NA_VALUE) < K_ZERO);
-        if (neg) report(m.err, 0x04u, 2, i);
-        else if (isnan(eta) || isinf(eta) || isnan(evapo) || isinf(evapo) || isnan(trans) || isinf(trans))
-            report(m.err, 0x08u, 3, i);
+        report_w(m.err, neg, 0x04u, 2, i);
+        report_w(m.err, !neg && (isnan(eta) || isinf(eta) || isnan(evapo) || isinf(evapo) || isnan(trans) || isinf(trans)),
+                 0x08u, 3, i);
         st1<VAR>(&m.e_ic[cur_e ^ 1][i], eic);
         if (DIAG) { dg.q_es[i] = Es; dg.q_eu[i] = Eu; dg.q_eg[i] = Eg; dg.q_tu[i] = Tu; dg.q_tg[i] = Tg;
                     dg.q_eta[i] = eta; dg.i_beta[i] = ibeta; }
@@ -86,7 +86,7 @@ shud_ele_kernel(DevMesh m, YView Y, double *__restrict__ dy, int n_compute, int 
 
     // ---- updateElement (Element.cpp:347-384) ----
     const double ekh = eff_kh(ugw, aq, m.macD[i], m.macKsatH[i], m.vAreaF[i], m.KsatH[i]);
-    if (ekh < 0. || ekh > 1e9) report(m.err, 0x02u, 1, i);
+    report_w(m.err, ekh < 0. || ekh > 1e9, 0x02u, 1, i);
     double deficit = aq - ugw;
     const double kmax = infK * (1. - hA) + macKV * hA;
     double theta, satn, satkr;
@@ -222,7 +222,7 @@ shud_ele_kernel(DevMesh m, YView Y, double *__restrict__ dy, int n_compute, int 
         sumsub += qsb;
         if (DIAG) { dg.qele_surf[j * NEl + i] = qsf; dg.qele_sub[j * NEl + i] = qsb; }
     }
-    if (MODE == 0 && nan_q) report(m.err, 0x01u, 0, i);
+    if (MODE == 0) report_w(m.err, nan_q, 0x01u, 0, i);
 
     // ---- f_applyDY element part (MD_f.cpp:88-131 / MD_f_omp.cpp:26-46) ----
     const double area = ld1<VAR>(&m.area[i]);
@@ -245,7 +245,6 @@ shud_ele_kernel(DevMesh m, YView Y, double *__restrict__ dy, int n_compute, int 
 // ===================================================================================
 // river kernel
 // ===================================================================================
-struct RivGeom { double csarea, csperem, topw, toparea; };
 
 // River.cpp:49-62 updateRiver + River.hpp:115-127
 __device__ __forceinline__ RivGeom riv_geom(const DevMesh &m, int r, double y) {

@@ -6,6 +6,37 @@
 #include <stdint.h>
 #include "shud_dev.h"
 
+// SHUD_ABL (timing-only ablation builds, never shipped): bit 0 pow, 1 cos, 2 cbrt, 3 division, 4 sqrt are
+// replaced by a single cheap op so their share of the element kernel's time can be measured.
+#ifndef SHUD_ABL
+#define SHUD_ABL 0
+#endif
+#if SHUD_ABL & 1
+#define SPOW(a, b) ((a) * (b))
+#else
+#define SPOW(a, b) pow(a, b)
+#endif
+#if SHUD_ABL & 2
+#define SCOS(a) (a)
+#else
+#define SCOS(a) cos(a)
+#endif
+#if SHUD_ABL & 4
+#define SCBRT(a) (a)
+#else
+#define SCBRT(a) cbrt(a)
+#endif
+#if SHUD_ABL & 8
+#define SDIV(a, b) ((a) * (b))
+#else
+#define SDIV(a, b) ((a) / (b))
+#endif
+#if SHUD_ABL & 16
+#define SSQRT(a) (a)
+#else
+#define SSQRT(a) sqrt(a)
+#endif
+
 namespace shud {
 
 // ---- constants: src/Model/Macros.hpp:46-77 ----
@@ -21,20 +52,20 @@ namespace shud {
 // functions.hpp:117-123 (NOT fmin/fmax: NaN behaviour must match)
 __device__ __forceinline__ double rmin(double a, double b) { return (a > b ? b : a); }
 __device__ __forceinline__ double rmax(double a, double b) { return (a < b ? b : a); }
-__device__ __forceinline__ double pow23(double x) { double t = cbrt(x); return t * t; }
+__device__ __forceinline__ double pow23(double x) { double t = SCBRT(x); return t * t; }
 
 // Equations.hpp:54-63
 __device__ __forceinline__ double manning(double A, double n, double R, double S) {
-    if (S > 0) return sqrt(S) * A * pow23(R) / n;
-    return -1.0 * sqrt(-S) * A * pow23(R) / n;
+    if (S > 0) return SDIV(SSQRT(S) * A * pow23(R), n);
+    return SDIV(-1.0 * SSQRT(-S) * A * pow23(R), n);
 }
 // Equations.cpp:116-134 (range check reported through *bad)
 __device__ __forceinline__ double eff_kh(double ygw, double aq, double macd, double kmac, double af,
                                          double kmx) {
     double e;
     if (macd <= K_ZERO || ygw < aq - macd) e = kmx;
-    else if (ygw > aq) e = (kmac * macd * af + kmx * (aq - macd * af)) / aq;
-    else e = (kmac * (ygw - (aq - macd)) * af + kmx * (aq - macd + (ygw - (aq - macd)) * (1 - af))) / ygw;
+    else if (ygw > aq) e = SDIV(kmac * macd * af + kmx * (aq - macd * af), aq);
+    else e = SDIV(kmac * (ygw - (aq - macd)) * af + kmx * (aq - macd + (ygw - (aq - macd)) * (1 - af)), ygw);
     return e;
 }
 // MD_RiverFlux.cpp:65-98
@@ -45,13 +76,13 @@ __device__ __forceinline__ double weir_jtoi(double zi, double yi, double zj, dou
         y = hi - zbank;
         if ((y > 0.) & (yj > thr)) {
             if (hi > zbank) y = dh;
-            Q = cwr * sqrt(2. * K_GRAV * y) * width * y * 60.;
+            Q = cwr * SSQRT(2. * K_GRAV * y) * width * y * 60.;
         } else Q = 0.;
     } else {
         y = hi - zbank;
         if (y > 0. && yi > thr) {
             if (hj > zbank) y = -dh;
-            Q = -1. * cwr * sqrt(2. * K_GRAV * y) * width * y * 60.;
+            Q = -1. * cwr * SSQRT(2. * K_GRAV * y) * width * y * 60.;
         } else Q = 0.;
     }
     return Q;
@@ -64,9 +95,9 @@ __device__ __forceinline__ double r2e_gw(double yr, double zr, double ye, double
     double he = ye + ze, hr = yr + zr, dh = hr - he, A, Q = 0.;
     if (dh > K_ZERO) {
         A = (he > zr) ? (yr + (he - zr)) * .5 * L : yr * L;
-        Q = (yr < K_EPSILON) ? 0. : A * K * (dh / D);
+        Q = (yr < K_EPSILON) ? 0. : A * K * SDIV(dh, D);
     } else if (dh < -K_ZERO) {
-        if (ye > K_ZERO) { A = (yr + (he - zr)) * .5 * L; Q = A * K * (dh / D); }
+        if (ye > K_ZERO) { A = (yr + (he - zr)) * .5 * L; Q = A * K * SDIV(dh, D); }
     }
     return Q;
 }
@@ -96,10 +127,20 @@ __device__ __forceinline__ int block_id() {
     return blockIdx.x;
 }
 
-// record an error: bit in flags, lowest index per bit
-__device__ __forceinline__ void report(DevErr *e, uint32_t bit, int slot, int idx) {
-    atomicOr(&e->flags, bit);
-    atomicMin(&e->first_index[slot], idx);
+struct RivGeom { double csarea, csperem, topw, toparea; };
+
+// record an error / warning, aggregated per wave: one lane (the lowest flagged lane = lowest element index
+// of the wave, since lanes map to consecutive indices) does the atomics for the whole wave, so inputs that
+// flag millions of elements cost one atomic per wave instead of serialising on one address.  Must be
+// reached by every active lane (it is a __ballot).
+__device__ __forceinline__ void report_w(DevErr *e, bool c, uint32_t bit, int slot, int idx, bool count = false) {
+    const unsigned long long mask = __ballot(c);
+    if (mask == 0ULL) return;
+    if ((int)__lane_id() == __ffsll((long long)mask) - 1) {
+        atomicOr(&e->flags, bit);
+        atomicMin(&e->first_index[slot], idx);
+        if (count) atomicAdd(&e->n_warn, (unsigned long long)__popcll(mask));
+    }
 }
 
 // uYgw after f_update's BC logic (MD_update.cpp:114-125 / MD_f_omp.cpp:119-128)

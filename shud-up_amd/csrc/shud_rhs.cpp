@@ -76,7 +76,6 @@ struct shud_rhs {
     long long ncalls = 0;
     int variant = 0;                     // element-kernel build variant (SHUD_RHS_ELE_VARIANT, A/B only)
     bool packed = false;                 // class-table / 16-byte-record layout in use (DevPacked)
-    int pk_waves = 0;                    // SHUD_RHS_PK_WAVES (A/B only)
     DevPacked dp{};
     int n_classes = 0;
     bool fu_unit[2] = {true, true};      // fu_Surf / fu_Sub are all 1.0 (cryosphere off): not read
@@ -149,7 +148,8 @@ extern "C" const char *shud_rhs_last_error_string(void) { return g_last_error.c_
 // create
 // ---------------------------------------------------------------------------------------------
 static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, const std::vector<int> &eflags,
-                        const std::vector<int> &seg_off);
+                        const std::vector<int> &seg_off, const std::vector<int> &up_off,
+                        const std::vector<int> &up_idx);
 
 static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, const ShudRhsOptions *opt,
                  const ShudPartition *part) {
@@ -165,7 +165,6 @@ static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, cons
     h->n_segghost = part ? part->n_segghost_ele : 0;
     h->n_own_riv = part ? part->n_own_riv : NR;
     if (const char *v = getenv("SHUD_RHS_ELE_VARIANT")) h->variant = atoi(v);
-    if (const char *v = getenv("SHUD_RHS_PK_WAVES")) h->pk_waves = atoi(v);
     if (h->n_own < 0 || h->n_own + h->n_segghost > NE || h->n_own_riv < 0 || h->n_own_riv > NR)
         return fail(SHUD_ERR_ARG, "partition counts inconsistent with mesh sizes");
 
@@ -344,7 +343,7 @@ static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, cons
         UP(rseg_off, rseg_off.data(), rseg_off.size()); UP(rseg_pos, rseg_pos.data(), rseg_pos.size());
     }
 #undef UP
-    if ((rc = build_packed(h, m, p, eflags, seg_off))) return rc;
+    if ((rc = build_packed(h, m, p, eflags, seg_off, up_off, up_idx))) return rc;
     if ((rc = h->dalloc(&h->d_err, 1))) return rc;
     d.err = h->d_err;
     HIP_TRY(hipHostMalloc((void **)&h->h_err, sizeof(DevErr), hipHostMallocDefault));
@@ -359,7 +358,8 @@ static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, cons
 // Packed class layout (shud_dev.h DevPacked).  Returns 0 with h->packed set, 0 with h->packed clear when
 // the mesh does not qualify (the SoA kernel is used), or an error code.
 static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, const std::vector<int> &eflags,
-                        const std::vector<int> &seg_off) {
+                        const std::vector<int> &seg_off, const std::vector<int> &up_off,
+                        const std::vector<int> &up_idx) {
     const char *env = getenv("SHUD_RHS_PACKED");
     if ((env && env[0] == '0') || h->variant) return 0;
     const int NE = m->num_ele;
@@ -371,8 +371,14 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
             const double want = nb >= 0 ? 0.5 * (m->rough[i] + m->rough[nb]) : m->rough[i];
             if (!(m->avg_rough[(size_t)j * NE + i] == want)) return 0;
         }
-    for (int i = 0; i < NE; i++)
+    // identities the packed record relies on (else the SoA kernel runs): AquiferDepth == z_surf - z_bottom
+    // (InitElement after rmSinks, Model_Data.cpp:262-264), |iBC| fits int8, <= 63 segments per element
+    for (int i = 0; i < NE; i++) {
+        if (!(p->aquifer_depth[i] == m->z_surf[i] - m->z_bottom[i])) return 0;
+        const int ibc = m->ibc ? m->ibc[i] : 0;
+        if (ibc > 127 || ibc < -127) return 0;
         if (seg_off[i + 1] - seg_off[i] > 63) return 0;
+    }
     // distinct parameter tuples -> class ids
     std::vector<std::vector<double>> table;           // [class][field]
     std::vector<int> cls(NE);
@@ -390,7 +396,7 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         std::string k((const char *)r.data(), r.size() * sizeof(double));
         auto it = ids.find(k);
         if (it == ids.end()) {
-            if ((int)table.size() >= (1 << 20)) return 0;
+            if ((int)table.size() >= 65536) return 0;
             it = ids.emplace(k, (int)table.size()).first;
             table.push_back(r);
         }
@@ -400,42 +406,95 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     std::vector<double> ctab((size_t)CF_COUNT * ncls);
     for (int c = 0; c < ncls; c++)
         for (int f = 0; f < CF_COUNT; f++) ctab[(size_t)f * ncls + c] = table[c][f];
-    std::vector<double2> zz(NE), aqk(NE), e01(NE), e2a(NE), d01(NE);
-    std::vector<double> d2(NE);
+    std::vector<double2> zz(NE), ged(3 * (size_t)NE);
     std::vector<int4> meta(NE);
+    std::vector<int> sfirst(NE);
     for (int i = 0; i < NE; i++) {
         zz[i] = make_double2(m->z_surf[i], m->z_bottom[i]);
         const int nseg = seg_off[i + 1] - seg_off[i];
-        const unsigned fl = (unsigned)(eflags[i] & 0x3ffff) | ((unsigned)nseg << 18);
-        const unsigned long long bits = ((unsigned long long)(unsigned)cls[i] << 32) | fl;
-        double bd;
-        memcpy(&bd, &bits, 8);
-        aqk[i] = make_double2(p->aquifer_depth[i], bd);
-        meta[i] = make_int4(m->nabr[i], m->nabr[(size_t)NE + i], m->nabr[2 * (size_t)NE + i], seg_off[i]);
-        e01[i] = make_double2(m->edge[i], m->edge[(size_t)NE + i]);
-        e2a[i] = make_double2(m->edge[2 * (size_t)NE + i], m->area[i]);
-        d01[i] = make_double2(m->dist2nabor[i], m->dist2nabor[(size_t)NE + i]);
-        d2[i] = m->dist2nabor[2 * (size_t)NE + i];
+        const int ibc = (int8_t)(eflags[i] & 0xff);
+        const unsigned cf = (unsigned)(ibc & 0xff) | ((unsigned)((eflags[i] >> 16) & 3) << 8) |
+                            ((unsigned)nseg << 10) | ((unsigned)cls[i] << 16);
+        meta[i] = make_int4(m->nabr[i], m->nabr[(size_t)NE + i], m->nabr[2 * (size_t)NE + i], (int)cf);
+        for (int j = 0; j < 3; j++)
+            ged[(size_t)j * NE + i] = make_double2(m->edge[(size_t)j * NE + i], m->dist2nabor[(size_t)j * NE + i]);
+        sfirst[i] = seg_off[i];
     }
     int rc;
     DevPacked &P = h->dp;
-    double *ctab_d; double2 *zz_d, *aqk_d, *e01_d, *e2a_d, *d01_d; double *d2_d; int4 *meta_d;
+    double *ctab_d, *area_d; double2 *zz_d, *ged_d; int4 *meta_d; int *sf_d;
     if ((rc = h->upload(&ctab_d, ctab.data(), ctab.size()))) return rc;
     if ((rc = h->upload(&zz_d, zz.data(), NE))) return rc;
-    if ((rc = h->upload(&aqk_d, aqk.data(), NE))) return rc;
     if ((rc = h->upload(&meta_d, meta.data(), NE))) return rc;
-    if ((rc = h->upload(&e01_d, e01.data(), NE))) return rc;
-    if ((rc = h->upload(&e2a_d, e2a.data(), NE))) return rc;
-    if ((rc = h->upload(&d01_d, d01.data(), NE))) return rc;
-    if ((rc = h->upload(&d2_d, d2.data(), NE))) return rc;
-    P.ctab = ctab_d; P.ncls = ncls; P.zz = zz_d; P.aqk = aqk_d; P.meta = meta_d; P.ge01 = e01_d; P.ge2a = e2a_d; P.gd01 = d01_d;
-    P.gd2 = d2_d;
+    if ((rc = h->upload(&ged_d, ged.data(), ged.size()))) return rc;
+    if ((rc = h->upload(&area_d, m->area, NE))) return rc;
+    if ((rc = h->upload(&sf_d, sfirst.data(), NE))) return rc;
+    P.ctab = ctab_d; P.ncls = ncls; P.zz = zz_d; P.meta = meta_d; P.ged = ged_d; P.area = area_d;
+    P.seg_first = sf_d;
+    {   // element-sorted segment records with their reach's statics (seg_perm: element-sorted -> reference)
+        const int NSg = m->num_seg;
+        std::vector<double2> lc(NSg), dk(NSg);
+        std::vector<int2> rb(NSg);
+        std::vector<double> bt(NSg);
+        for (int k = 0; k < NSg; k++) {
+            const int s = h->seg_perm[k], r = m->seg_riv[s];
+            lc[k] = make_double2(m->seg_length[s], m->seg_cwr[s]);
+            dk[k] = make_double2(m->riv_depth[r], m->riv_ksath[r]);
+            rb[k] = make_int2(r, m->riv_bc ? m->riv_bc[r] : 0);
+            bt[k] = m->riv_bedthick[r];
+        }
+        double2 *lc_d, *dk_d; int2 *rb_d; double *bt_d;
+        if ((rc = h->upload(&lc_d, lc.data(), NSg))) return rc;
+        if ((rc = h->upload(&dk_d, dk.data(), NSg))) return rc;
+        if ((rc = h->upload(&rb_d, rb.data(), NSg))) return rc;
+        if ((rc = h->upload(&bt_d, bt.data(), NSg))) return rc;
+        P.sg_lc = lc_d; P.sg_dk = dk_d; P.sg_rb = rb_d; P.sg_bt = bt_d;
+    }
     if ((rc = h->upload(&P.s_np, (const double2 *)nullptr, NE))) return rc;
     if ((rc = h->upload(&P.s_tl, (const double2 *)nullptr, NE))) return rc;
     if ((rc = h->upload(&P.cs[0], (const double2 *)nullptr, NE))) return rc;
     if ((rc = h->upload(&P.cs[1], (const double2 *)nullptr, NE))) return rc;
     std::vector<double2> ones(NE, make_double2(1.0, 1.0));
     if ((rc = h->upload(&P.s_fu, ones.data(), NE))) return rc;
+
+    // ---- segments in reach order (stable: reference order inside a reach) and reach records ----
+    const int NS = m->num_seg, NR = m->num_riv;
+    std::vector<int> rorder(NS);
+    std::iota(rorder.begin(), rorder.end(), 0);
+    std::stable_sort(rorder.begin(), rorder.end(), [&](int a, int b) { return m->seg_riv[a] < m->seg_riv[b]; });
+    std::vector<int> rstart(NR, 0), rcnt(NR, 0);
+    for (int q = NS - 1; q >= 0; q--) rstart[m->seg_riv[rorder[q]]] = q;
+    for (int s = 0; s < NS; s++) rcnt[m->seg_riv[s]]++;
+    std::vector<double2> ra(NR), rb(NR), rcc(NR), rd(NR);
+    std::vector<int4> ri(NR), ru(NR);
+    const int nor = h->n_own_riv;
+    for (int r = 0; r < NR; r++) {
+        ra[r] = make_double2(m->riv_bottom_width[r], m->riv_bankslope[r]);
+        rb[r] = make_double2(m->riv_length[r], m->riv_bed_slope[r]);
+        rcc[r] = make_double2(m->riv_dist2down[r], m->riv_avg_rough[r]);
+        rd[r] = make_double2(m->riv_depth[r], 0.0);
+        ri[r] = make_int4(m->riv_down[r], m->riv_bc ? m->riv_bc[r] : 0, rstart[r], rcnt[r]);
+        int4 u = make_int4(0, 0, 0, 0);
+        if (r < nor) {
+            const int n = up_off[r + 1] - up_off[r];
+            if (n <= 3) {
+                int v[3] = {0, 0, 0};
+                for (int k = 0; k < n; k++) v[k] = up_idx[up_off[r] + k];
+                u = make_int4(v[0], v[1], v[2], n);
+            } else {
+                u = make_int4(0, 0, 0, -1);
+            }
+        }
+        ru[r] = u;
+    }
+    double2 *ra_d, *rb_d, *rc_d, *rd_d; int4 *ri_d, *ru_d;
+    if ((rc = h->upload(&ra_d, ra.data(), NR))) return rc;
+    if ((rc = h->upload(&rb_d, rb.data(), NR))) return rc;
+    if ((rc = h->upload(&rc_d, rcc.data(), NR))) return rc;
+    if ((rc = h->upload(&rd_d, rd.data(), NR))) return rc;
+    if ((rc = h->upload(&ri_d, ri.data(), NR))) return rc;
+    if ((rc = h->upload(&ru_d, ru.data(), NR))) return rc;
+    P.rv_a = ra_d; P.rv_b = rb_d; P.rv_c = rc_d; P.rv_d = rd_d; P.rv_i = ri_d; P.rv_u = ru_d;
     h->n_classes = ncls;
     h->packed = true;
     return 0;
@@ -596,14 +655,17 @@ static void launch_ele(shud_rhs *h, const double *y, double *dy, int cur, int cu
     YView Y{y, h->d_gele, h->d_griv, h->n_own, h->n_own_riv};
     if (h->packed && !h->variant)
         launch_element_kernel_packed(h->dm, h->dp, Y, dy, h->n_own + h->n_segghost, cur, h->mode, h->open, diag,
-                                     h->fu_unit[0] && h->fu_unit[1], h->dd, h->stream, h->pk_waves);
+                                     h->fu_unit[0] && h->fu_unit[1], h->dd, h->stream);
     else
         launch_element_kernel(h->dm, Y, dy, h->n_own + h->n_segghost, cur, cur_e, h->mode, h->open, diag, h->dd,
                               h->stream, h->variant);
 }
 static void launch_riv(shud_rhs *h, const double *y, double *dy, bool diag) {
     YView Y{y, h->d_gele, h->d_griv, h->n_own, h->n_own_riv};
-    launch_river_kernel(h->dm, Y, dy, h->mode, diag, h->dd, h->stream);
+    if (h->packed && !h->variant)
+        launch_river_kernel_packed(h->dm, h->dp, Y, dy, h->mode, diag, h->dd, h->stream);
+    else
+        launch_river_kernel(h->dm, Y, dy, h->mode, diag, h->dd, h->stream);
 }
 static void launch_all(shud_rhs *h, const double *y, double *dy, int cur, int cur_e, bool diag) {
     launch_ele(h, y, dy, cur, cur_e, diag);
@@ -774,13 +836,14 @@ extern "C" int shud_rhs_sync_diagnostics(shud_rhs_t h, ShudFluxOut *o) {
     std::vector<double> tmp;
     if (o->qseg_surf || o->qseg_sub) tmp.resize(std::max<size_t>(NS, 1));
     HIP_TRY(hipStreamSynchronize(h->stream));
+    const std::vector<int> &perm = h->seg_perm;
     if (o->qseg_surf) {
         HIP_TRY(hipMemcpy(tmp.data(), h->dm.qseg_surf, NS * sizeof(double), hipMemcpyDeviceToHost));
-        for (size_t k = 0; k < NS; k++) o->qseg_surf[h->seg_perm[k]] = tmp[k];
+        for (size_t k = 0; k < NS; k++) o->qseg_surf[perm[k]] = tmp[k];
     }
     if (o->qseg_sub) {
         HIP_TRY(hipMemcpy(tmp.data(), h->dm.qseg_sub, NS * sizeof(double), hipMemcpyDeviceToHost));
-        for (size_t k = 0; k < NS; k++) o->qseg_sub[h->seg_perm[k]] = tmp[k];
+        for (size_t k = 0; k < NS; k++) o->qseg_sub[perm[k]] = tmp[k];
     }
     return SHUD_OK;
 }

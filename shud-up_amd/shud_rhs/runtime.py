@@ -12,7 +12,8 @@ import numpy as np
 from . import abi
 
 _LIB = None
-LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "libshud_rhs.so")
+LIB_PATH = os.environ.get("SHUD_RHS_LIB") or os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "libshud_rhs.so")   # env: A/B builds only
 
 
 class ShudRhsError(RuntimeError):
