@@ -6,7 +6,7 @@ ccw-like river density, seed 12345), seeded random state y and ET-step inputs, s
 shud`) semantics.  One "step" = one RHS evaluation f(t, y, ydot) with y / ydot resident in HBM.
 N = 1: the whole mesh on one GPU.  N > 1 (torch.distributed.run, one process per GPU): the same 10M mesh
 partitioned by RCB across the N ranks, ghost states exchanged by RCCL (grouped send/recv over xGMI) inside
-every RHS call; value = NumEle_total x K / max-over-ranks time ("scaling": "strong", total work fixed).
+every RHS call; value = NumEle_total x K / max-over-ranks time ("scaling": "strong": the 10M mesh is fixed).
 
 Prints ONE JSON line on rank 0 with roofline (dominant kernel: shud_ele_kernel, HIP-event timed on the
 stream it runs on) and cpu_baseline (the CPU restatement oracle on this host's cores, bounded sample).
@@ -36,7 +36,7 @@ def log(*a):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--n-ele", type=int, default=10_000_000)
     ap.add_argument("--mode", choices=["serial", "omp"], default="serial")
@@ -135,7 +135,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_step,
         "higher_is_better": True,
-        "scaling": "strong" if world > 1 else "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded jittered-grid Delaunay mesh + river tree, random y and ET-step inputs)",
@@ -157,6 +157,10 @@ def main():
         },
         "cpu_baseline": None,
     }
+    # the practical HBM ceiling on this box: a STREAM-copy (torch's device copy kernel, 2 GiB -> 2 GiB)
+    sc = stream_copy_gbs(local)
+    out["roofline"]["stream_copy_GBs"] = sc
+    out["roofline"]["frac_of_stream_copy"] = achieved / 1e9 / sc if sc else None
     pmc = os.path.join(ROOT, "profiles", "pmc_summary.json")
     if os.path.exists(pmc) and world == 1:
         try:
@@ -187,6 +191,32 @@ def main():
     h.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def stream_copy_gbs(dev, n=1 << 28, reps=20):
+    """STREAM copy (shud-up_amd/libshud_stream.so: 16-B non-temporal loads/stores, grid-stride), 2 GiB -> 2 GiB,
+    HIP-event timed on torch's current stream: the practical HBM ceiling of this box."""
+    import ctypes
+    import torch
+    lib = ctypes.CDLL(os.path.join(ROOT, "shud-up_amd", "libshud_stream.so"))
+    lib.shud_stream_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    a = torch.ones(n, dtype=torch.float64, device=f"cuda:{dev}")
+    b = torch.empty_like(a)
+    st = torch.cuda.current_stream().cuda_stream
+    for _ in range(3):
+        lib.shud_stream_copy(a.data_ptr(), b.data_ptr(), 8 * n, st)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        lib.shud_stream_copy(a.data_ptr(), b.data_ptr(), 8 * n, st)
+    e1.record()
+    torch.cuda.synchronize()
+    ok = bool(torch.equal(a[:1024], b[:1024]))
+    gbs = 2 * 8 * n * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return gbs if ok else None
 
 
 def cpu_baseline(gm, y, mode, budget_s):

@@ -56,6 +56,14 @@ __device__ __forceinline__ double ugw_pk(const DevMesh &m, double ygw_raw, int i
     return m.ugw_stale[j];
 }
 
+#ifndef SHUD_ET_EARLY
+#define SHUD_ET_EARLY 1
+#endif
+#ifndef SHUD_EDGE_PIPE
+#define SHUD_EDGE_PIPE 0
+#endif
+struct EdgeIn { double2 g, nzz; int ncf; double nsf, ngw; };
+
 // class table staged in LDS (record-major [class][field], 144 B per class) when it has <= LDS_CLS_MAX classes:
 // the 18 + 3x5 class lookups per element become LDS reads with immediate offsets instead of dependent L2 trips
 #ifndef SHUD_LDS_CLS_MAX
@@ -88,6 +96,13 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     const double ysf_raw = Y.sf(i), yus_raw = Y.us(i), ygw_raw = Y.gw(i);
     const int cf = mt.w;
     const int cid = cf_class(cf), ibc = cf_ibc(cf);
+#if SHUD_ET_EARLY
+    const double2 snp = ldnt2(&p.s_np[i]), stl = ldnt2(&p.s_tl[i]);
+    const double etp = ldnt(&m.etp[i]);
+    double2 fu;
+    if (FU1) { fu.x = 1.0; fu.y = 1.0; } else fu = ldnt2(&p.s_fu[i]);
+    const double2 csv = ldnt2(&p.cs[cur][i]);
+#endif
 #define CL(f) (LCT ? lct[cid * CF_COUNT + CF_##f] : p.ctab[CF_##f * ncls + cid])
 
     // ---- f_update ----
@@ -115,11 +130,13 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         }
     }
 
+#if !SHUD_ET_EARLY
     const double2 snp = ldnt2(&p.s_np[i]), stl = ldnt2(&p.s_tl[i]);
     const double etp = ldnt(&m.etp[i]);
     double2 fu;
     if (FU1) { fu.x = 1.0; fu.y = 1.0; } else fu = ldnt2(&p.s_fu[i]);
     const double2 csv = ldnt2(&p.cs[cur][i]);
+#endif
     const int sfirst = p.seg_first[i];
     const int iss = cf_iss(cf), nseg = cf_nseg(cf);
     const double infD = CL(infD), ThS = CL(ThetaS), ThR = CL(ThetaR);
@@ -206,6 +223,22 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     const double dgw_head = q_rech - q_exfil;
     if (i < nown) __builtin_nontemporal_store(SDIV(q_infil - q_rech - Eu - Tu, CL(Sy)), &dy[nown + i]);
 
+#if SHUD_EDGE_PIPE
+    auto load_edge = [&](int j) {
+        EdgeIn e;
+        const int nb = j == 0 ? mt.x : j == 1 ? mt.y : mt.z;
+        const int nc = nb >= 0 ? nb : i;                  // boundary edge: harmless in-bounds loads
+        e.g = ldnt2(&p.ged[(size_t)j * NEl + i]);
+        e.nzz = p.zz[nc];
+        e.ncf = p.meta[nc].w;
+        e.nsf = Y.sf(nc);
+        e.ngw = Y.gw(nc);
+        return e;
+    };
+#if SHUD_EDGE_PIPE == 2
+    const EdgeIn e0 = load_edge(0);                       // in flight across the segment loop
+#endif
+#endif
     // ---- own river segments (fun_Seg_surface / fun_Seg_sub) and Qe2r (PassValue) ----
     const double dep = CL(depression), rgh = CL(rough);
     double qe2r_surf = 0., qe2r_sub = 0.;
@@ -222,8 +255,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
             const double rdep = dk.x, L = lc.x;
             const double qs = weir_jtoi(zs, isf_seg, zs - rdep, yr, zs + 0.0, lc.y, L, dep);
             const double qg = r2e_gw(yr, zs - rdep, ugw, zb, ekh, dk.y, L, bt) * fu_sub;
-            m.qseg_surf[k] = qs;           // element-sorted: consecutive lanes write consecutive k
-            m.qseg_sub[k] = qg;
+            p.qseg2[k] = make_double2(qs, qg);    // element-sorted: consecutive lanes, consecutive k
             qe2r_surf += -qs;
             qe2r_sub += -qg;
         }
@@ -238,9 +270,24 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     // ---- fun_Ele_surface / fun_Ele_sub, one edge per (rolled) iteration (MD_ElementFlux.cpp:35-156) ----
     // each edge's neighbour data is loaded at the top of its iteration; keeping the loop rolled holds the
     // kernel at 96 VGPRs = 5 waves/SIMD (all three edges in flight at once needs ~145 = 3 waves: slower)
+#if SHUD_EDGE_PIPE == 1
+    const EdgeIn e0 = load_edge(0);
+#endif
     double sumsurf = qe2r_surf, sumsub = qe2r_sub;     // QeleSurfTot = Qe2r + sum_j QeleSurf[j]
     bool nan_q = false;
     const double isf = usf < 0. ? 0. : usf;
+#if SHUD_EDGE_PIPE
+    // software-pipelined: edge j+1's neighbour records are in flight while edge j is computed
+    EdgeIn ein = e0;
+#pragma unroll 1
+    for (int j = 0; j < 3; j++) {
+        const int nb = j == 0 ? mt.x : j == 1 ? mt.y : mt.z;
+        const EdgeIn e = ein;
+        ein = load_edge(j < 2 ? j + 1 : 2);
+        const double2 g = e.g, nzz = e.nzz;
+        const int ncf = e.ncf;
+        const double nsf_raw = e.nsf, ngw_raw = e.ngw;
+#else
 #pragma unroll 1
     for (int j = 0; j < 3; j++) {
         const int nb = j == 0 ? mt.x : j == 1 ? mt.y : mt.z;
@@ -249,6 +296,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         const double2 nzz = p.zz[nc];
         const int ncf = p.meta[nc].w;
         const double nsf_raw = Y.sf(nc), ngw_raw = Y.gw(nc);
+#endif
         const double B = g.x, d2n = g.y;
         double qsf = 0., qsb = 0.;
         if (nb >= 0) {
@@ -420,12 +468,19 @@ shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         }
     }
     // segment sums, ascending reference segment order (MD_f.cpp:228-235), gathered from the element-sorted
-    // fluxes (scattered 8-B writes from the element kernel cost more than these gathers)
+    // fluxes (scattered 8-B writes from the element kernel cost more than these gathers).  Batches of 8:
+    // all index loads, then all gathers, are in flight together; the adds stay in segment order
     double qsurf = 0., qsub = 0.;
-    for (int k = ii.z, k1 = ii.z + ii.w; k < k1; k++) {
-        const int ps = m.rseg_pos[k];
-        qsurf += m.qseg_surf[ps];
-        qsub += m.qseg_sub[ps];
+    for (int k0 = ii.z, k1 = ii.z + ii.w; k0 < k1; k0 += 8) {
+        int ps[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) ps[j] = m.rseg_pos[k0 + j < k1 ? k0 + j : k0];
+        double2 qv[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) qv[j] = p.qseg2[ps[j]];
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+            if (k0 + j < k1) { qsurf += qv[j].x; qsub += qv[j].y; }
     }
     const double qbc = (q.bc < 0) ? m.rqbc[-q.bc] : 0.0;
     double dv;

@@ -449,6 +449,7 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         if ((rc = h->upload(&rb_d, rb.data(), NSg))) return rc;
         if ((rc = h->upload(&bt_d, bt.data(), NSg))) return rc;
         P.sg_lc = lc_d; P.sg_dk = dk_d; P.sg_rb = rb_d; P.sg_bt = bt_d;
+        if ((rc = h->upload(&P.qseg2, (const double2 *)nullptr, NSg))) return rc;
     }
     if ((rc = h->upload(&P.s_np, (const double2 *)nullptr, NE))) return rc;
     if ((rc = h->upload(&P.s_tl, (const double2 *)nullptr, NE))) return rc;
@@ -837,6 +838,15 @@ extern "C" int shud_rhs_sync_diagnostics(shud_rhs_t h, ShudFluxOut *o) {
     if (o->qseg_surf || o->qseg_sub) tmp.resize(std::max<size_t>(NS, 1));
     HIP_TRY(hipStreamSynchronize(h->stream));
     const std::vector<int> &perm = h->seg_perm;
+    if (h->packed && !h->variant && NS && (o->qseg_surf || o->qseg_sub)) {
+        std::vector<double2> q2(NS);
+        HIP_TRY(hipMemcpy(q2.data(), h->dp.qseg2, NS * sizeof(double2), hipMemcpyDeviceToHost));
+        for (size_t k = 0; k < NS; k++) {
+            if (o->qseg_surf) o->qseg_surf[perm[k]] = q2[k].x;
+            if (o->qseg_sub) o->qseg_sub[perm[k]] = q2[k].y;
+        }
+        return SHUD_OK;
+    }
     if (o->qseg_surf) {
         HIP_TRY(hipMemcpy(tmp.data(), h->dm.qseg_surf, NS * sizeof(double), hipMemcpyDeviceToHost));
         for (size_t k = 0; k < NS; k++) o->qseg_surf[perm[k]] = tmp[k];
