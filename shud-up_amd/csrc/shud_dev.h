@@ -48,7 +48,19 @@ struct DevMesh {
 // wave-instruction gathering one field for 64 lanes touches a few cache lines, not one per class)
 enum ClassField {
     CF_macD, CF_macKsatH, CF_vAreaF, CF_KsatH, CF_KsatV, CF_infKsatV, CF_hAreaF, CF_macKsatV, CF_ThetaS,
-    CF_ThetaR, CF_Beta, CF_infD, CF_Sy, CF_RzD, CF_VegFrac, CF_ImpAF, CF_depression, CF_rough, CF_COUNT
+    CF_ThetaR, CF_Beta, CF_infD, CF_Sy, CF_RzD, CF_VegFrac, CF_ImpAF, CF_depression, CF_rough,
+    CF_NPRIMARY,
+    // derived per class on the host, in the kernel's own operation order (bit-identical by construction)
+    CF_fcmr = CF_NPRIMARY,  // ThetaS * 0.75 - ThetaR
+    CF_dTh,                 // ThetaS - ThetaR
+    CF_ex1, CF_ex2,         // Beta / (Beta - 1),  (Beta - 1) / Beta
+    CF_vb, CF_pj,           // 1 - VegFrac,  1 - ImpAF
+    CF_omh,                 // 1 - hAreaF
+    CF_kmax,                // infKsatV * (1 - hAreaF) + macKsatV * hAreaF
+    CF_ekA, CF_ekB,         // infKsatV * (1 - hAreaF),  hAreaF * macKsatV
+    // correctly rounded reciprocals of the class-constant divisors (cdiv, shud_physics.h)
+    CF_r_fcmr, CF_r_dTh, CF_r_infD, CF_r_Sy,
+    CF_COUNT
 };
 struct DevPacked {
     const double *ctab;     // [CF_COUNT][ncls]

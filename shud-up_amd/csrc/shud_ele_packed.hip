@@ -75,7 +75,7 @@ template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT>
 __global__ void __launch_bounds__(256, 5)
 shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int n_compute, int cur,
                        DevDiag dg) {
-    __shared__ double lct[LCT ? CF_COUNT * (LDS_CLS_MAX > 0 ? LDS_CLS_MAX : 1) : 1];
+    extern __shared__ double lct[];                       // ncls * CF_COUNT doubles when LCT
     const int ncls = p.ncls;
     if (LCT) {
         for (int t = threadIdx.x; t < ncls * CF_COUNT; t += blockDim.x) {
@@ -104,6 +104,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     const double2 csv = ldnt2(&p.cs[cur][i]);
 #endif
 #define CL(f) (LCT ? lct[cid * CF_COUNT + CF_##f] : p.ctab[CF_##f * ncls + cid])
+#define CDIV(a, F) CDIV_(a, CL(F), CL(r_##F))
 
     // ---- f_update ----
     double usf = ysf_raw, uus = yus_raw;
@@ -120,12 +121,11 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     {
         const double ThS = CL(ThetaS), ThR = CL(ThetaR);
         if (deficit <= 0.) { deficit = 0.; satn = 1.; theta = ThS; }
-        else { theta = SDIV(uus, deficit) * ThS; satn = SDIV(theta - ThR, ThS - ThR); }
+        else { theta = SDIV(uus, deficit) * ThS; satn = CDIV(theta - ThR, dTh); }
         if (satn > 0.99) { satn = 1.0; satkr = 1.0; theta = ThS; }
         else if (satn <= K_ZERO) { satn = 0.; satkr = 0.; theta = ThR; }
         else {   // satKfun, Equations.cpp:136-141
-            const double n = CL(Beta);
-            const double tmp = -1. + SPOW(1. - SPOW(satn, SDIV(n, n - 1.)), SDIV(n - 1., n));
+            const double tmp = -1. + SPOW(1. - SPOW(satn, CL(ex1)), CL(ex2));   // n/(n-1), (n-1)/n
             satkr = SSQRT(satn) * tmp * tmp;
         }
     }
@@ -139,19 +139,18 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
 #endif
     const int sfirst = p.seg_first[i];
     const int iss = cf_iss(cf), nseg = cf_nseg(cf);
-    const double infD = CL(infD), ThS = CL(ThetaS), ThR = CL(ThetaR);
-    const double infK = CL(infKsatV), hA = CL(hAreaF), macKV = CL(macKsatV);
+    const double infD = CL(infD), ThR = CL(ThetaR);
+    const double infK = CL(infKsatV);
     const double fu_surf = fu.x, fu_sub = fu.y;
 
     // ---- f_etFlux (MD_ET.cpp:343-404), serial semantics only (reads the previous call's u_satn) ----
     double Es = 0., Eu = 0., Eg = 0., Tu = 0., Tg = 0., eic = csv.y, ibeta = 0.;
     if (MODE == 0) {
         const double satn_prev = csv.x;
-        const double vf = CL(VegFrac), va = vf, vb = 1. - vf, pj = 1. - CL(ImpAF);
+        const double va = CL(VegFrac), vb = CL(vb), pj = CL(pj);
         const double pet = snp.y, ptr = stl.x;
         {
-            double fc = ThS * K_FC_RATIO;
-            double b = SDIV(satn_prev * (ThS - ThR) - ThR, fc - ThR);
+            double b = CDIV(satn_prev * CL(dTh) - ThR, fcmr);           // fc = ThS * 0.75
             b = rmin(rmax(0., b), 1.);
             ibeta = 0.5 * (1 - SCOS(K_PI * b));
         }
@@ -180,7 +179,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
                     dg.q_eta[i] = eta; dg.i_beta[i] = ibeta; }
     }
     stnt2(&p.cs[cur ^ 1][i], satn, eic);
-    const double kmax = infK * (1. - hA) + macKV * hA;
+    const double kmax = CL(kmax);
 
     // ---- Flux_Infiltration (Element.cpp:271-303) ----
     double qi = 0., qex = 0.;
@@ -189,11 +188,11 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         if (ugw + uus > aq || deficit < uus) {
             qex = SDIV(fabs(ugw + uus - aq), aq) * kmax;
         } else if (av > 0. && deficit > infD) {
-            const double grad = 1. + SDIV(av, infD);
+            const double grad = 1. + CDIV(av, infD);
             double ek;
-            if (av > kmax) ek = infK * (1 - hA) + hA * macKV * satn;
-            else if (av > infK) ek = satkr * infK * (1 - hA) + hA * macKV * satn;
-            else ek = satkr * infK * (1 - hA);
+            if (av > kmax) ek = CL(ekA) + CL(ekB) * satn;
+            else if (av > infK) ek = satkr * infK * CL(omh) + CL(ekB) * satn;
+            else ek = satkr * infK * CL(omh);
             qi = rmin(av, rmax(0., grad * ek));
         }
     }
@@ -205,7 +204,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         if (!(ugw > aq - infD && uus < deficit)) {
             double grad = 0.;
             if (theta > ThR && !(uus <= K_EPSILON)) {
-                grad = SDIV(theta - ThR, ThS * K_FC_RATIO - ThR);
+                grad = CDIV(theta - ThR, fcmr);
                 grad = rmax(grad, 0.);
             }
             if (!(infK <= 0. || KV <= 0.)) {
@@ -221,7 +220,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     // dgw = (recharge - exfil) - Qsub/area - Eg - Tg.  Ends the ET/vertical live ranges early.
     const double dsf_head = snp.x - q_infil + q_exfil;
     const double dgw_head = q_rech - q_exfil;
-    if (i < nown) __builtin_nontemporal_store(SDIV(q_infil - q_rech - Eu - Tu, CL(Sy)), &dy[nown + i]);
+    if (i < nown) __builtin_nontemporal_store(CDIV(q_infil - q_rech - Eu - Tu, Sy), &dy[nown + i]);
 
 #if SHUD_EDGE_PIPE
     auto load_edge = [&](int j) {
@@ -360,7 +359,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     else if (ibc < 0) dgw += SDIV(m.eqbc[-ibc], area);
     if (iss == 1) dsf += 0.0 / area;                          // QSS is never assigned: 0
     else if (iss == 2) dgw += 0.0 / area;
-    dgw = SDIV(dgw, CL(Sy));
+    dgw = CDIV(dgw, Sy);
 #undef CL
     __builtin_nontemporal_store(dsf, &dy[i]);
     __builtin_nontemporal_store(dgw, &dy[2 * nown + i]);
@@ -532,7 +531,8 @@ static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, doubl
                      const DevDiag &dg, hipStream_t s) {
     int nb = (n + 255) / 256;
     nb = (nb + 7) / 8 * 8;                  // block_id<1> deals blocks to XCDs in contiguous chunks
-    hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT>), dim3(nb), dim3(256), 0, s, m, p, Y, dy, n,
+    const size_t lds = LCT ? (size_t)p.ncls * CF_COUNT * sizeof(double) : 0;
+    hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT>), dim3(nb), dim3(256), lds, s, m, p, Y, dy, n,
                        cur, dg);
 }
 

@@ -39,6 +39,25 @@
 
 namespace shud {
 
+// a / b for a class-constant divisor b with its host-computed, correctly rounded reciprocal rb (SHUD_CDIV=1):
+// q0 = a*rb is within 1 ulp of a/b, the residual a - q0*b is exact in one fma, and one fma correction then
+// rounds to nearest exactly like IEEE division (Markstein's theorem; round-to-nearest, no under/overflow).
+// Exact, zero, infinite and NaN residuals keep q0 (signed zeros and infinities as a/b gives them).
+// SHUD_CDIV=0 uses the plain division.
+#ifndef SHUD_CDIV
+#define SHUD_CDIV 0
+#endif
+__device__ __forceinline__ double cdiv(double a, double b, double rb) {
+    const double q0 = a * rb;
+    const double e = __builtin_fma(-q0, b, a);
+    return (e == 0. || !__builtin_isfinite(e)) ? q0 : __builtin_fma(e, rb, q0);
+}
+#if SHUD_CDIV && !(SHUD_ABL & 8)
+#define CDIV_(a, b, rb) cdiv(a, b, rb)
+#else
+#define CDIV_(a, b, rb) SDIV(a, b)
+#endif
+
 // ---- constants: src/Model/Macros.hpp:46-77 ----
 #define K_EPSILON 0.005
 #define K_ZERO 1.0e-10

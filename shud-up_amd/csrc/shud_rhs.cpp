@@ -384,7 +384,7 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     std::vector<int> cls(NE);
     std::unordered_map<std::string, int> ids;
     const double dep_default = 0.0002;
-    std::vector<double> r(CF_COUNT);
+    std::vector<double> r(CF_NPRIMARY);
     for (int i = 0; i < NE; i++) {
         r[CF_macD] = p->macD[i]; r[CF_macKsatH] = p->macKsatH[i]; r[CF_vAreaF] = p->geo_vAreaF[i];
         r[CF_KsatH] = p->KsatH[i]; r[CF_KsatV] = p->KsatV[i]; r[CF_infKsatV] = p->infKsatV[i];
@@ -404,8 +404,26 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     }
     const int ncls = (int)table.size();
     std::vector<double> ctab((size_t)CF_COUNT * ncls);
-    for (int c = 0; c < ncls; c++)
-        for (int f = 0; f < CF_COUNT; f++) ctab[(size_t)f * ncls + c] = table[c][f];
+    for (int c = 0; c < ncls; c++) {
+        std::vector<double> &t = table[c];
+        t.resize(CF_COUNT);
+        // same expressions, same order as the element kernel (-ffp-contract=off on both sides)
+        t[CF_fcmr] = t[CF_ThetaS] * 0.75 - t[CF_ThetaR];
+        t[CF_dTh] = t[CF_ThetaS] - t[CF_ThetaR];
+        t[CF_ex1] = t[CF_Beta] / (t[CF_Beta] - 1.);
+        t[CF_ex2] = (t[CF_Beta] - 1.) / t[CF_Beta];
+        t[CF_vb] = 1. - t[CF_VegFrac];
+        t[CF_pj] = 1. - t[CF_ImpAF];
+        t[CF_omh] = 1. - t[CF_hAreaF];
+        t[CF_kmax] = t[CF_infKsatV] * (1. - t[CF_hAreaF]) + t[CF_macKsatV] * t[CF_hAreaF];
+        t[CF_ekA] = t[CF_infKsatV] * (1. - t[CF_hAreaF]);
+        t[CF_ekB] = t[CF_hAreaF] * t[CF_macKsatV];
+        t[CF_r_fcmr] = 1. / t[CF_fcmr];
+        t[CF_r_dTh] = 1. / t[CF_dTh];
+        t[CF_r_infD] = 1. / t[CF_infD];
+        t[CF_r_Sy] = 1. / t[CF_Sy];
+        for (int f = 0; f < CF_COUNT; f++) ctab[(size_t)f * ncls + c] = t[f];
+    }
     std::vector<double2> zz(NE), ged(3 * (size_t)NE);
     std::vector<int4> meta(NE);
     std::vector<int> sfirst(NE);
