@@ -111,7 +111,7 @@ struct YView {
 
 void launch_element_kernel(const DevMesh &m, const YView &Y, double *dy, int n_compute, int cur, int cur_e,
                            int mode, bool open, bool diag, const DevDiag &dg, hipStream_t s, int variant = 0);
-void launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int n_compute,
+void launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1,
                                   int cur, int mode, bool open, bool diag, bool fu_unit, const DevDiag &dg,
                                   hipStream_t s);
 void launch_river_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int mode,

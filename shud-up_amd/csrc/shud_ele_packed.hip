@@ -73,7 +73,7 @@ constexpr int LDS_CLS_MAX = SHUD_LDS_CLS_MAX;
 
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT>
 __global__ void __launch_bounds__(256, 5)
-shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int n_compute, int cur,
+shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int i0, int n_compute, int cur,
                        DevDiag dg) {
     extern __shared__ double lct[];                       // ncls * CF_COUNT doubles when LCT
     const int ncls = p.ncls;
@@ -84,7 +84,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         }
         __syncthreads();
     }
-    const int i = block_id<1>() * blockDim.x + threadIdx.x;
+    const int i = i0 + block_id<1>() * blockDim.x + threadIdx.x;   // elements [i0, n_compute)
     if (i >= n_compute) return;
     const int NEl = m.num_ele;
     const int nown = Y.n_own;
@@ -527,21 +527,21 @@ shud_pack_step_kernel(DevMesh m, DevPacked p, int n, int cur, unsigned what) {
 }
 
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT>
-static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int n, int cur,
+static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1, int cur,
                      const DevDiag &dg, hipStream_t s) {
-    int nb = (n + 255) / 256;
+    int nb = (i1 - i0 + 255) / 256;
     nb = (nb + 7) / 8 * 8;                  // block_id<1> deals blocks to XCDs in contiguous chunks
     const size_t lds = LCT ? (size_t)p.ncls * CF_COUNT * sizeof(double) : 0;
-    hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT>), dim3(nb), dim3(256), lds, s, m, p, Y, dy, n,
-                       cur, dg);
+    hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT>), dim3(nb), dim3(256), lds, s, m, p, Y, dy,
+                       i0, i1, cur, dg);
 }
 
-void launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int n_compute,
+void launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1,
                                   int cur, int mode, bool open, bool diag, bool fu_unit, const DevDiag &dg,
                                   hipStream_t s) {
-    if (n_compute <= 0) return;
-#define LP(MO, OP, DI, FU) do { if (p.ncls <= LDS_CLS_MAX) launch_p<MO, OP, DI, FU, true>(m, p, Y, dy, n_compute, cur, dg, s); \
-                                 else launch_p<MO, OP, DI, FU, false>(m, p, Y, dy, n_compute, cur, dg, s); } while (0)
+    if (i1 <= i0) return;
+#define LP(MO, OP, DI, FU) do { if (p.ncls <= LDS_CLS_MAX) launch_p<MO, OP, DI, FU, true>(m, p, Y, dy, i0, i1, cur, dg, s); \
+                                 else launch_p<MO, OP, DI, FU, false>(m, p, Y, dy, i0, i1, cur, dg, s); } while (0)
 #define LFU(MO, OP, DI) do { if (fu_unit) LP(MO, OP, DI, true); else LP(MO, OP, DI, false); } while (0)
 #define LDI(MO, OP) do { if (diag) LFU(MO, OP, true); else LFU(MO, OP, false); } while (0)
 #define LOP(MO) do { if (open) LDI(MO, true); else LDI(MO, false); } while (0)

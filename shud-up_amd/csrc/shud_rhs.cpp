@@ -61,6 +61,7 @@ int fail(int code, const char *fmt, ...) {
 struct shud_rhs {
     int NE = 0, NR = 0, NS = 0;          // local totals (incl. ghosts)
     int n_own = 0, n_segghost = 0, n_own_riv = 0;
+    int n_int = 0;                       // partitioned: owned prefix independent of ghost data
     int mode = SHUD_MODE_SERIAL;
     bool open = false;
     bool check_errors = true;
@@ -100,6 +101,8 @@ struct shud_rhs {
     int rank = 0, nranks = 1;
     bool use_nccl = false;
     ncclComm_t comm = nullptr;
+    hipStream_t s_comm = nullptr;        // RCCL halo exchange, overlapped with the interior element kernel
+    hipEvent_t ev_pack = nullptr, ev_comm = nullptr;
     std::vector<int> esend_off, erecv_off, rsend_off, rrecv_off;
     int *d_esend_idx = nullptr, *d_rsend_idx = nullptr;
     int n_esend = 0, n_rsend = 0, n_eghost = 0, n_rghost = 0;
@@ -232,6 +235,19 @@ static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, cons
         if (m->seg_ele[s] >= ncomp && m->seg_riv[s] < h->n_own_riv)
             return fail(SHUD_ERR_ARG, "segment %d of an owned reach belongs to a non-computed ghost element", s);
     h->seg_perm = order;
+    // ---- partitioned: owned elements [0, n_int) read no ghost data (all lateral neighbours owned, all their
+    // segments' reaches owned); they run while the halo exchange is in flight (eval_device) ----
+    h->n_int = 0;
+    if (part) {
+        int i = 0;
+        for (; i < h->n_own; i++) {
+            bool dep = false;
+            for (int j = 0; j < 3 && !dep; j++) dep = m->nabr[(size_t)j * NE + i] >= h->n_own;
+            for (int k = seg_off[i]; k < seg_off[i + 1] && !dep; k++) dep = seg_riv[k] >= h->n_own_riv;
+            if (dep) break;
+        }
+        h->n_int = i;
+    }
     // ---- per owned reach: its segments (ascending reference order) and upstream reaches ----
     std::vector<int> rseg_off(h->n_own_riv + 1, 0), rseg_pos;
     for (int s = 0; s < NS; s++)
@@ -551,6 +567,9 @@ static int setup_partition(shud_rhs *h, const ShudPartition *part) {
         memcpy(&id, part->nccl_unique_id, sizeof(id));
         h->use_nccl = true;
         NCCL_TRY(ncclCommInitRank(&h->comm, P, id, part->rank));
+        HIP_TRY(hipStreamCreateWithFlags(&h->s_comm, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&h->ev_pack, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&h->ev_comm, hipEventDisableTiming));
     }
     return 0;
 }
@@ -559,7 +578,11 @@ static void destroy_handle(shud_rhs *h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->s_comm) (void)hipStreamSynchronize(h->s_comm);
     if (h->comm) ncclCommDestroy(h->comm);
+    if (h->ev_pack) (void)hipEventDestroy(h->ev_pack);
+    if (h->ev_comm) (void)hipEventDestroy(h->ev_comm);
+    if (h->s_comm) (void)hipStreamDestroy(h->s_comm);
     for (void *p : h->allocs) (void)hipFree(p);
     if (h->h_err) (void)hipHostFree(h->h_err);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
@@ -651,29 +674,36 @@ extern "C" int shud_rhs_set_step_inputs(shud_rhs_t h, const ShudStepInputs *in) 
 // ---------------------------------------------------------------------------------------------
 // eval
 // ---------------------------------------------------------------------------------------------
+// pack the owned states peers need (main stream), then the grouped RCCL send/recv on the comm stream:
+// ev_comm marks the ghost buffers filled.
 static int exchange(shud_rhs *h, const double *y) {
     if (!h->partitioned) return 0;
     launch_pack_kernel(y, h->n_own, h->n_own_riv, h->d_esend_idx, h->n_esend, h->d_rsend_idx, h->n_rsend,
                        h->d_esend, h->d_rsend, h->stream);
     if (!h->use_nccl) return 0;      // external transport (tests): caller moved the buffers
+    HIP_TRY(hipEventRecord(h->ev_pack, h->stream));
+    HIP_TRY(hipStreamWaitEvent(h->s_comm, h->ev_pack, 0));
     NCCL_TRY(ncclGroupStart());
     for (int p = 0; p < h->nranks; p++) {
         if (p == h->rank) continue;
         size_t se = h->esend_off[p + 1] - h->esend_off[p], re = h->erecv_off[p + 1] - h->erecv_off[p];
         size_t sr = h->rsend_off[p + 1] - h->rsend_off[p], rr = h->rrecv_off[p + 1] - h->rrecv_off[p];
-        if (se) NCCL_TRY(ncclSend(h->d_esend + 3 * (size_t)h->esend_off[p], 3 * se, ncclDouble, p, h->comm, h->stream));
-        if (re) NCCL_TRY(ncclRecv(h->d_gele + 3 * (size_t)h->erecv_off[p], 3 * re, ncclDouble, p, h->comm, h->stream));
-        if (sr) NCCL_TRY(ncclSend(h->d_rsend + h->rsend_off[p], sr, ncclDouble, p, h->comm, h->stream));
-        if (rr) NCCL_TRY(ncclRecv(h->d_griv + h->rrecv_off[p], rr, ncclDouble, p, h->comm, h->stream));
+        if (se) NCCL_TRY(ncclSend(h->d_esend + 3 * (size_t)h->esend_off[p], 3 * se, ncclDouble, p, h->comm, h->s_comm));
+        if (re) NCCL_TRY(ncclRecv(h->d_gele + 3 * (size_t)h->erecv_off[p], 3 * re, ncclDouble, p, h->comm, h->s_comm));
+        if (sr) NCCL_TRY(ncclSend(h->d_rsend + h->rsend_off[p], sr, ncclDouble, p, h->comm, h->s_comm));
+        if (rr) NCCL_TRY(ncclRecv(h->d_griv + h->rrecv_off[p], rr, ncclDouble, p, h->comm, h->s_comm));
     }
     NCCL_TRY(ncclGroupEnd());
+    HIP_TRY(hipEventRecord(h->ev_comm, h->s_comm));
     return 0;
 }
 
-static void launch_ele(shud_rhs *h, const double *y, double *dy, int cur, int cur_e, bool diag) {
+static void launch_ele(shud_rhs *h, const double *y, double *dy, int cur, int cur_e, bool diag, int i0 = 0,
+                       int i1 = -1) {
     YView Y{y, h->d_gele, h->d_griv, h->n_own, h->n_own_riv};
+    if (i1 < 0) i1 = h->n_own + h->n_segghost;
     if (h->packed && !h->variant)
-        launch_element_kernel_packed(h->dm, h->dp, Y, dy, h->n_own + h->n_segghost, cur, h->mode, h->open, diag,
+        launch_element_kernel_packed(h->dm, h->dp, Y, dy, i0, i1, cur, h->mode, h->open, diag,
                                      h->fu_unit[0] && h->fu_unit[1], h->dd, h->stream);
     else
         launch_element_kernel(h->dm, Y, dy, h->n_own + h->n_segghost, cur, cur_e, h->mode, h->open, diag, h->dd,
@@ -705,14 +735,29 @@ static int read_err(shud_rhs *h) {
 
 static const uint32_t kFatal = SHUD_EF_NAN_QELE | SHUD_EF_EFFKH | SHUD_EF_ET_NEG | SHUD_EF_ET_NAN;
 
+// partitioned handles: the interior elements [0, n_int) run while the halo exchange is in flight (RCCL on
+// s_comm); boundary + ghost elements and the reaches wait for it.  Unpartitioned: one launch each.
+static int launch_split(shud_rhs *h, const double *y, double *dy) {
+    if (h->partitioned && h->packed && !h->variant && h->n_int > 0) {
+        launch_ele(h, y, dy, h->cur, h->cur_e, false, 0, h->n_int);
+        if (h->use_nccl) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_comm, 0));
+        launch_ele(h, y, dy, h->cur, h->cur_e, false, h->n_int, h->n_own + h->n_segghost);
+        launch_riv(h, y, dy, false);
+    } else {
+        if (h->use_nccl) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_comm, 0));
+        launch_all(h, y, dy, h->cur, h->cur_e, false);
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
 static int eval_device(shud_rhs *h, double t, const double *y, double *dy) {
     (void)t;
     int rc = exchange(h, y);
     if (rc) return rc;
     h->last_cur = h->cur;
     h->last_cur_e = h->cur_e;
-    launch_all(h, y, dy, h->cur, h->cur_e, false);
-    HIP_TRY(hipGetLastError());
+    if ((rc = launch_split(h, y, dy))) return rc;
     flip(h);
     h->last_y = y;
     h->have_last = true;
@@ -923,8 +968,8 @@ extern "C" int shud_rhs_eval_compute(shud_rhs_t h, double t, const double *d_y, 
     if (!h) return fail(SHUD_ERR_ARG, "null argument");
     h->last_cur = h->cur;
     h->last_cur_e = h->cur_e;
-    launch_all(h, d_y, d_ydot, h->cur, h->cur_e, false);
-    HIP_TRY(hipGetLastError());
+    int rc = launch_split(h, d_y, d_ydot);
+    if (rc) return rc;
     flip(h);
     h->last_y = d_y;
     h->have_last = true;
@@ -945,8 +990,9 @@ extern "C" int shud_rhs_time_kernels(shud_rhs_t h, double t, const double *d_y, 
         int k = 0;
         HIP_TRY(hipEventRecord(E[k++], h->stream));
         if (h->partitioned) {
-            int rc = exchange(h, d_y);
+            int rc = exchange(h, d_y);        // serialized here (no overlap) so each phase is timed alone
             if (rc) return rc;
+            if (h->use_nccl) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_comm, 0));
             HIP_TRY(hipEventRecord(E[k++], h->stream));
         }
         launch_ele(h, d_y, d_ydot, h->cur, h->cur_e, false);

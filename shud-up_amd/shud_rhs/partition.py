@@ -5,7 +5,8 @@ centroids (vertex weight 1 + number of river segments, as §8e asks of the dual-
 elements -> part; each reach -> the part owning most of its segments' elements (ties: lowest part; a reach
 without segments follows its first element-owning neighbour reach, else part 0).
 
-Local numbering of rank p:  elements [owned (global order) | ghosts grouped by source rank (global order)],
+Local numbering of rank p:  elements [owned interior | owned boundary | ghosts grouped by source rank], each
+group in global order (boundary = reads a ghost neighbour or a ghost reach; the interior runs during the halo exchange),
 reaches [owned | ghosts grouped by source rank], segments = every segment whose element or reach is owned,
 in global segment order.  Ghost elements = lateral neighbours of owned elements + elements of segments of
 owned reaches; they carry replicated static data, step inputs and carried state, and the element kernel
@@ -118,6 +119,14 @@ def _ghost_sets(m, ele_part, riv_part, r):
     up = np.nonzero((m.riv_down >= 0) & own_r_mask[np.where(m.riv_down >= 0, m.riv_down, 0)])[0]
     ghost_r = np.union1d(np.union1d(m.seg_riv[segs], rd[rd >= 0]), up)
     ghost_r = ghost_r[~own_r_mask[ghost_r]]
+    # owned elements: [interior | boundary] (stable).  Boundary = reads ghost data: a lateral neighbour or a
+    # segment reach owned elsewhere.  The interior prefix runs while the halo exchange is in flight.
+    nb = m.nabr.reshape(3, -1)[:, own_e]
+    dep = ((nb >= 0) & ~own_e_mask[np.where(nb >= 0, nb, 0)]).any(axis=0)
+    own_seg = own_e_mask[m.seg_ele]
+    bad_seg_ele = m.seg_ele[own_seg & ~own_r_mask[m.seg_riv]]
+    dep |= np.isin(own_e, bad_seg_ele)
+    own_e = np.concatenate([own_e[~dep], own_e[dep]])
     return own_e, own_r, segs, ghost_e, ghost_r
 
 

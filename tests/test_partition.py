@@ -66,6 +66,25 @@ def test_k_rank_simulation_bit_identical(nranks, mode):
                 assert np.array_equal(got, want), f"rank {r} call {call}"
 
 
+@pytest.mark.parametrize("nranks", [2, 4, 8])
+def test_interior_prefix(nranks):
+    """Owned elements are numbered [interior | boundary]: the interior prefix reads no ghost data (the GPU
+    handle runs it while the halo exchange is in flight) and it is most of the owned set."""
+    m, _ = cases.variant(20000, seed=5)
+    _, _, plans = partition.build_plans(m, nranks)
+    for r in range(nranks):
+        lm, part = partition.local_model(m, plans[r], r, nranks)
+        own = part.n_own_ele
+        nab = lm.nabr.reshape(3, -1)[:, :own]
+        dep = (nab >= own).any(0)
+        bad = np.zeros(lm.num_ele, bool)
+        np.logical_or.at(bad, lm.seg_ele[lm.seg_riv >= part.n_own_riv], True)
+        dep |= bad[:own]
+        n_int = int(np.argmax(dep)) if dep.any() else own
+        assert not dep[:n_int].any() and dep[n_int:].all(), "owned elements not ordered [interior | boundary]"
+        assert n_int >= 0.8 * own
+
+
 def test_rcb_balance():
     m = cases.variant(20000, seed=3)[0]
     ep, rp = partition.assign_owners(m, 8)
