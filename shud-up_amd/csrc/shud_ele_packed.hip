@@ -70,17 +70,20 @@ struct EdgeIn { double2 g, nzz; int ncf; double nsf, ngw; };
 #define SHUD_LDS_CLS_MAX 128
 #endif
 constexpr int LDS_CLS_MAX = SHUD_LDS_CLS_MAX;
+// odd record stride (in 8-B words): lanes of one wave reading the same field of different classes land on
+// different LDS banks (an even stride of 32 words put every class on one bank: ~960 conflict cycles/wave)
+constexpr int CF_LDS_STRIDE = CF_COUNT | 1;
 
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT>
 __global__ void __launch_bounds__(256, 5)
 shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int i0, int n_compute, int cur,
                        DevDiag dg) {
-    extern __shared__ double lct[];                       // ncls * CF_COUNT doubles when LCT
+    extern __shared__ double lct[];                       // ncls * CF_LDS_STRIDE doubles when LCT
     const int ncls = p.ncls;
     if (LCT) {
         for (int t = threadIdx.x; t < ncls * CF_COUNT; t += blockDim.x) {
             const int c = t / CF_COUNT, f = t - c * CF_COUNT;
-            lct[t] = p.ctab[f * ncls + c];
+            lct[c * CF_LDS_STRIDE + f] = p.ctab[f * ncls + c];
         }
         __syncthreads();
     }
@@ -103,7 +106,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     if (FU1) { fu.x = 1.0; fu.y = 1.0; } else fu = ldnt2(&p.s_fu[i]);
     const double2 csv = ldnt2(&p.cs[cur][i]);
 #endif
-#define CL(f) (LCT ? lct[cid * CF_COUNT + CF_##f] : p.ctab[CF_##f * ncls + cid])
+#define CL(f) (LCT ? lct[cid * CF_LDS_STRIDE + CF_##f] : p.ctab[CF_##f * ncls + cid])
 #define CDIV(a, F) CDIV_(a, CL(F), CL(r_##F))
 
     // ---- f_update ----
@@ -300,7 +303,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         double qsf = 0., qsb = 0.;
         if (nb >= 0) {
             const int cn = cf_class(ncf);
-#define CN(f) (LCT ? lct[cn * CF_COUNT + CF_##f] : p.ctab[CF_##f * ncls + cn])
+#define CN(f) (LCT ? lct[cn * CF_LDS_STRIDE + CF_##f] : p.ctab[CF_##f * ncls + cn])
             double nsf = nsf_raw;
             if (MODE == 1) nsf = (nsf >= 0.) ? nsf : 0.;
             nsf = nsf < 0. ? 0. : nsf;
@@ -531,7 +534,7 @@ static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, doubl
                      const DevDiag &dg, hipStream_t s) {
     int nb = (i1 - i0 + 255) / 256;
     nb = (nb + 7) / 8 * 8;                  // block_id<1> deals blocks to XCDs in contiguous chunks
-    const size_t lds = LCT ? (size_t)p.ncls * CF_COUNT * sizeof(double) : 0;
+    const size_t lds = LCT ? (size_t)p.ncls * CF_LDS_STRIDE * sizeof(double) : 0;
     hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT>), dim3(nb), dim3(256), lds, s, m, p, Y, dy,
                        i0, i1, cur, dg);
 }
