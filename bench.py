@@ -70,7 +70,8 @@ def main():
 
     stream = torch.cuda.current_stream()
     if world > 1:
-        _, _, plans = partition.build_plans(gm, world)
+        ele_part, _, plans = partition.build_plans(gm, world)
+        cut_e, cut_s = partition.edge_cut(gm, ele_part)
         lm, part = partition.local_model(gm, plans[rank], rank, world)
         uid = [runtime.nccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
@@ -78,7 +79,8 @@ def main():
         h = runtime.RhsHandle(lm, mode=mode, device=local, stream=stream.cuda_stream, partition=part)
         y_loc = partition.local_state(y_glob, gm, part)
         model = lm
-        log(f"[bench] rank0 partition: own {part.n_own_ele} ele / {part.n_own_riv} riv, "
+        log(f"[bench] RCB {world}-way: edge cut {cut_e} mesh edges, {cut_s} river segments; rank0 "
+            f"own {part.n_own_ele} ele / {part.n_own_riv} riv, "
             f"ghosts {lm.num_ele - part.n_own_ele} ele / {lm.num_riv - part.n_own_riv} riv")
     else:
         h = runtime.RhsHandle(gm, mode=mode, device=local, stream=stream.cuda_stream)
@@ -142,6 +144,7 @@ def main():
         "config": {"workload": f"syn-10M RHS ({args.mode} semantics)" if NE >= 9_000_000 else f"syn-{NE} RHS",
                    "num_ele": NE, "num_riv": NR, "num_seg": NS,
                    "parallelism": f"mesh-partition x{world} (RCB, RCCL halo)" if world > 1 else "single GPU",
+                   **({"edge_cut": cut_e, "segment_cut": cut_s} if world > 1 else {}),
                    "y_ydot": "device-resident"},
         "roofline": {
             "bound": "hbm",
@@ -237,10 +240,22 @@ def cpu_baseline(gm, y, mode, budget_s):
         el = time.perf_counter() - t0
         if el >= budget_s or n >= 40:
             break
-    return {"value": gm.num_ele * n / el, "unit": "element-flux-updates/s", "cores": threads,
-            "kind": "port",
-            "sample": f"{n} RHS calls of the CPU restatement (oracle/shud_oracle.c, OpenMP {threads} threads) on "
-                      f"the full syn-10M mesh, {el:.1f}s wall"}
+    out = {"value": gm.num_ele * n / el, "unit": "element-flux-updates/s", "cores": threads, "kind": "port",
+           "sample": f"{n} RHS calls of the CPU restatement (oracle/shud_oracle.c, OpenMP {threads} threads) on "
+                     f"the full syn-10M mesh, {el:.1f}s wall"}
+    # the same restatement on 1 thread (SURVEY §8d asks for both), a bounded sample of ~budget_s / 3
+    oracle.set_threads(1)
+    n1, t1 = 0, time.perf_counter()
+    while True:
+        o.eval(0.0, y)
+        n1 += 1
+        el1 = time.perf_counter() - t1
+        if el1 >= budget_s / 3 or n1 >= 10:
+            break
+    out["value_1thread"] = gm.num_ele * n1 / el1
+    out["sample_1thread"] = f"{n1} RHS calls on 1 thread, {el1:.1f}s wall"
+    oracle.set_threads(threads)
+    return out
 
 
 if __name__ == "__main__":

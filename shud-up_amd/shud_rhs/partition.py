@@ -130,6 +130,18 @@ def _ghost_sets(m, ele_part, riv_part, r):
     return own_e, own_r, segs, ghost_e, ghost_r
 
 
+def edge_cut(m, ele_part):
+    """Partition quality: #mesh edges whose two elements are on different parts, and #river
+    segments whose element and reach are owned by different parts."""
+    nab = m.nabr.reshape(3, -1)
+    i = np.broadcast_to(np.arange(m.num_ele), nab.shape)
+    ok = nab > i                          # each interior edge once
+    cut_e = int((ele_part[i[ok]] != ele_part[nab[ok]]).sum())
+    _, riv_part = assign_owners(m, int(ele_part.max()) + 1, ele_part)
+    cut_s = int((ele_part[m.seg_ele] != riv_part[m.seg_riv]).sum())
+    return cut_e, cut_s
+
+
 def build_plans(m, nparts, ele_part=None):
     """Global partition -> per-rank (local element order, local reach order, segment set, plan)."""
     ele_part, riv_part = assign_owners(m, nparts, ele_part)

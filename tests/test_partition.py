@@ -85,6 +85,18 @@ def test_interior_prefix(nranks):
         assert n_int >= 0.8 * own
 
 
+def test_edge_cut_counts():
+    m, _ = cases.variant(20000, seed=5)
+    one = np.zeros(m.num_ele, dtype=np.int32)
+    assert partition.edge_cut(m, one) == (0, 0)
+    ep, _, _ = partition.build_plans(m, 4)
+    ce, cs = partition.edge_cut(m, ep)
+    nab = m.nabr.reshape(3, -1)
+    brute = sum(1 for j in range(3) for i in range(m.num_ele)
+                if nab[j, i] > i and ep[i] != ep[nab[j, i]])
+    assert ce == brute and 0 < ce < 0.1 * m.num_ele and cs >= 0
+
+
 def test_rcb_balance():
     m = cases.variant(20000, seed=3)[0]
     ep, rp = partition.assign_owners(m, 8)
