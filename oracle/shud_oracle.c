@@ -838,3 +838,36 @@ void oracle_destroy(OracleModel *M) {
     for (; p <= end; p++) free(*p);
     free(M);
 }
+
+/* ===================== known-answer entry =====================
+ * oracle_kat(fn, in, n, out): the leaf equations above on n input tuples (row-major, kat_nin(fn) doubles
+ * each), one output per tuple.  The device side (shud-up_amd/csrc/shud_kat.hip) evaluates the same ids
+ * with the kernels' own device functions; tests/test_kat.py compares them on edge-case grids. */
+enum { KAT_MANNING, KAT_EFFKH, KAT_WEIR, KAT_R2E, KAT_SATK, KAT_SMS, KAT_DADY, KAT_AREA, KAT_PEREM, KAT_TOPW,
+       KAT_TOPAREA, KAT_COUNT };
+static const int kat_nin_tab[KAT_COUNT] = {4, 6, 8, 8, 2, 3, 3, 4, 4, 4, 4};
+int oracle_kat_nin(int fn) { return (fn >= 0 && fn < KAT_COUNT) ? kat_nin_tab[fn] : -1; }
+int oracle_kat(int fn, const double *in, int n, double *out) {
+    if (fn < 0 || fn >= KAT_COUNT) return -1;
+    const int k = kat_nin_tab[fn];
+    for (int t = 0; t < n; t++) {
+        const double *x = in + (size_t)t * k;
+        double r = 0.;
+        int bad = 0;
+        switch (fn) {
+            case KAT_MANNING: r = ManningEquation(x[0], x[1], x[2], x[3]); break;
+            case KAT_EFFKH: r = effKH(x[0], x[1], x[2], x[3], x[4], x[5], &bad); break;
+            case KAT_WEIR: r = WeirFlow_jtoi(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]); break;
+            case KAT_R2E: r = flux_R2E_GW(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]); break;
+            case KAT_SATK: r = satKfun(x[0], x[1]); break;
+            case KAT_SMS: r = SoilMoistureStress(x[0], x[1], x[2]); break;
+            case KAT_DADY: r = fun_dAtodY(x[0], x[1], x[2]); break;
+            case KAT_AREA: r = fixMaxValue(fun_CrossArea(x[3], x[0], x[1]), 0.); break;
+            case KAT_PEREM: r = fixMaxValue(fun_CrossPerem(x[3], x[0], x[1]), 0.); break;
+            case KAT_TOPW: r = fixMaxValue(fun_TopWidth(x[3], x[0], x[1]), 0.); break;
+            case KAT_TOPAREA: r = fixMaxValue(fun_EqWidth(x[3], x[0], x[1]) * x[2], 0.); break;
+        }
+        out[t] = r;
+    }
+    return 0;
+}

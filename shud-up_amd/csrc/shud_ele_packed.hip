@@ -128,8 +128,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         if (satn > 0.99) { satn = 1.0; satkr = 1.0; theta = ThS; }
         else if (satn <= K_ZERO) { satn = 0.; satkr = 0.; theta = ThR; }
         else {   // satKfun, Equations.cpp:136-141
-            const double tmp = -1. + SPOW(1. - SPOW(satn, CL(ex1)), CL(ex2));   // n/(n-1), (n-1)/n
-            satkr = SSQRT(satn) * tmp * tmp;
+            satkr = sat_kfun(satn, CL(ex1), CL(ex2));                    // n/(n-1), (n-1)/n
         }
     }
 
@@ -153,9 +152,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         const double va = CL(VegFrac), vb = CL(vb), pj = CL(pj);
         const double pet = snp.y, ptr = stl.x;
         {
-            double b = CDIV(satn_prev * CL(dTh) - ThR, fcmr);           // fc = ThS * 0.75
-            b = rmin(rmax(0., b), 1.);
-            ibeta = 0.5 * (1 - SCOS(K_PI * b));
+            ibeta = soil_moisture_stress(CDIV(satn_prev * CL(dTh) - ThR, fcmr));   // fc = ThS * 0.75
         }
         Es = rmin(rmax(0., usf), pet) * vb;
         if (Es < pet) {
@@ -384,21 +381,7 @@ __device__ __forceinline__ RivP riv_load(const DevPacked &p, int r) {
     o.down = ii.x; o.bc = ii.y;
     return o;
 }
-// River.cpp:49-62 updateRiver (pre-BC stage) + River.hpp:115-127
-__device__ __forceinline__ RivGeom riv_geom_p(const RivP &q, double y) {
-    RivGeom g;
-    const double topw = y * q.bs * 2.0 + q.w0;
-    const double a = y * (q.w0 + y * q.bs);
-    const double ys = y * q.bs;
-    const double per = 2.0 * sqrt(y * y + ys * ys) + q.w0;
-    const double eqw = 0.5 * ((y * q.bs * 2.0 + q.w0) + q.w0);
-    const double ta = eqw * q.len;
-    g.topw = (topw < 0.) ? 0. : topw;
-    g.csarea = (a < 0.) ? 0. : a;
-    g.csperem = (per < 0.) ? 0. : per;
-    g.toparea = (ta < 0.) ? 0. : ta;
-    return g;
-}
+__device__ __forceinline__ RivGeom riv_geom_p(const RivP &q, double y) { return riv_geom(q.w0, q.bs, q.len, y); }
 // stage after f_update's clamp + BC override; *yg = the value updateRiver() saw
 template <int MODE>
 __device__ __forceinline__ double riv_stage_p(const DevMesh &m, const YView &Y, int r, int bc, double *yg) {
@@ -490,13 +473,7 @@ shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     else if (MODE == 0) {   // MD_f.cpp:162-166
         dv = (-qup - qsurf - qsub - qdown + qbc) / q.len;
         if (dv < -1. * g.csarea) dv = -1. * g.csarea;
-        if (dv == 0.) dv = 0.;                                        // fun_dAtodY functions.hpp:141-153
-        else if (fabs(q.bs) < K_EPS_SLOPE) dv = dv / g.topw;
-        else {                                                        // Quadratic functions.hpp:125-139
-            const double sa = fabs(q.bs);
-            const double cc = g.topw * g.topw + 4 * sa * dv;
-            dv = (cc < K_ZERO) ? -1. * g.topw / (2. * sa) : (-g.topw + sqrt(cc)) / (2 * sa);
-        }
+        dv = da_to_dy(dv, g.topw, q.bs);                              // fun_dAtodY functions.hpp:125-153
     } else {                // MD_f_omp.cpp:59
         dv = (-qup - qsurf - qsub - qdown + qbc) / g.toparea;
     }

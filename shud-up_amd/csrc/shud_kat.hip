@@ -1,0 +1,61 @@
+// shud_kat.hip — known-answer harness (test infrastructure; not part of the RHS C-ABI):
+// evaluates the element/river kernels' own device leaf functions (shud_physics.h) on host-given input
+// tuples, ids and argument order as oracle_kat() (oracle/shud_oracle.c).  tests/test_kat.py compares.
+#include <hip/hip_runtime.h>
+#include <vector>
+#include "shud_physics.h"
+
+using namespace shud;
+
+enum { KAT_MANNING, KAT_EFFKH, KAT_WEIR, KAT_R2E, KAT_SATK, KAT_SMS, KAT_DADY, KAT_AREA, KAT_PEREM, KAT_TOPW,
+       KAT_TOPAREA, KAT_COUNT };
+static const int kat_nin_tab[KAT_COUNT] = {4, 6, 8, 8, 2, 3, 3, 4, 4, 4, 4};
+
+__global__ void kat_kernel(int fn, int k, const double *__restrict__ in, int n, double *__restrict__ out) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const double *x = in + (size_t)t * k;
+    double r = 0.;
+    switch (fn) {
+        case KAT_MANNING: r = manning(x[0], x[1], x[2], x[3]); break;
+        case KAT_EFFKH: r = eff_kh(x[0], x[1], x[2], x[3], x[4], x[5]); break;
+        case KAT_WEIR: r = weir_jtoi(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]); break;
+        case KAT_R2E: r = r2e_gw(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]); break;
+        case KAT_SATK: {                       // class exponents as the handle derives them (shud_rhs.cpp)
+            const double nb = x[1];
+            r = sat_kfun(x[0], nb / (nb - 1.), (nb - 1.) / nb);
+            break;
+        }
+        case KAT_SMS: {                        // dth and fcmr as the handle derives them
+            const double ths = x[0], thr = x[1];
+            r = soil_moisture_stress((x[2] * (ths - thr) - thr) / (ths * 0.75 - thr));
+            break;
+        }
+        case KAT_DADY: r = da_to_dy(x[0], x[1], x[2]); break;
+        case KAT_AREA: r = riv_geom(x[0], x[1], x[2], x[3]).csarea; break;
+        case KAT_PEREM: r = riv_geom(x[0], x[1], x[2], x[3]).csperem; break;
+        case KAT_TOPW: r = riv_geom(x[0], x[1], x[2], x[3]).topw; break;
+        case KAT_TOPAREA: r = riv_geom(x[0], x[1], x[2], x[3]).toparea; break;
+    }
+    out[t] = r;
+}
+
+extern "C" int shud_kat_nin(int fn) { return (fn >= 0 && fn < KAT_COUNT) ? kat_nin_tab[fn] : -1; }
+
+extern "C" int shud_kat_eval(int fn, const double *h_in, int n, double *h_out) {
+    if (fn < 0 || fn >= KAT_COUNT || n <= 0) return -1;
+    const int k = kat_nin_tab[fn];
+    double *d_in = nullptr, *d_out = nullptr;
+    if (hipMalloc(&d_in, sizeof(double) * k * (size_t)n) != hipSuccess) return -3;
+    if (hipMalloc(&d_out, sizeof(double) * (size_t)n) != hipSuccess) { (void)hipFree(d_in); return -3; }
+    int rc = 0;
+    if (hipMemcpy(d_in, h_in, sizeof(double) * k * (size_t)n, hipMemcpyHostToDevice) != hipSuccess) rc = -3;
+    if (!rc) {
+        hipLaunchKernelGGL(kat_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, fn, k, d_in, n, d_out);
+        if (hipGetLastError() != hipSuccess) rc = -3;
+    }
+    if (!rc && hipMemcpy(h_out, d_out, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess) rc = -3;
+    (void)hipFree(d_in);
+    (void)hipFree(d_out);
+    return rc;
+}

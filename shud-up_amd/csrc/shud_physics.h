@@ -147,6 +147,41 @@ __device__ __forceinline__ int block_id() {
 }
 
 struct RivGeom { double csarea, csperem, topw, toparea; };
+// _River::updateRiver (River.cpp:49-62) with fun_Cross* (River.hpp:115-127): geometry at stage y
+__device__ __forceinline__ RivGeom riv_geom(double w0, double bs, double len, double y) {
+    RivGeom g;
+    const double topw = y * bs * 2.0 + w0;
+    const double a = y * (w0 + y * bs);
+    const double ys = y * bs;
+    const double per = 2.0 * sqrt(y * y + ys * ys) + w0;
+    const double eqw = 0.5 * ((y * bs * 2.0 + w0) + w0);
+    const double ta = eqw * len;
+    g.topw = (topw < 0.) ? 0. : topw;
+    g.csarea = (a < 0.) ? 0. : a;
+    g.csperem = (per < 0.) ? 0. : per;
+    g.toparea = (ta < 0.) ? 0. : ta;
+    return g;
+}
+// satKfun, Equations.cpp:136-141, with the class exponents ex1 = n/(n-1), ex2 = (n-1)/n precomputed
+__device__ __forceinline__ double sat_kfun(double satn, double ex1, double ex2) {
+    const double tmp = -1. + SPOW(1. - SPOW(satn, ex1), ex2);
+    return SSQRT(satn) * tmp * tmp;
+}
+// SoilMoistureStress, is_sm_et.cpp:131-140 (truncated PI), with dth = ThetaS - ThetaR and
+// fcmr = ThetaS * 0.75 - ThetaR; b = (SatRatio * dth - ThetaR) / fcmr
+__device__ __forceinline__ double soil_moisture_stress(double b) {
+    b = rmin(rmax(0., b), 1.);
+    return 0.5 * (1 - SCOS(K_PI * b));
+}
+// fun_dAtodY + Quadratic, functions.hpp:125-153
+__device__ __forceinline__ double da_to_dy(double dA, double w_top, double s) {
+    if (dA == 0.) return 0.;
+    if (fabs(s) < K_EPS_SLOPE) return dA / w_top;
+    const double sa = fabs(s);
+    const double cc = w_top * w_top + 4 * sa * dA;
+    return (cc < K_ZERO) ? -1. * w_top / (2. * sa) : (-w_top + sqrt(cc)) / (2 * sa);
+}
+
 
 // record an error / warning, aggregated per wave: one lane (the lowest flagged lane = lowest element index
 // of the wave, since lanes map to consecutive indices) does the atomics for the whole wave, so inputs that

@@ -8,6 +8,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "shud-up_amd"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 GOLDEN = os.path.join(ROOT, "tests", "golden")
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+PKG_DIR = os.path.join(ROOT, "shud-up_amd")
 
 # GPU parity tolerance: |gpu - ref| <= RTOL*|ref| + ATOL per state.
 RTOL = 1e-12

@@ -1,0 +1,167 @@
+"""Leaf-equation known-answer tests on edge-case grids (tests/kat_grids.py).
+
+CPU: the oracle's C leaf functions (oracle_kat) against an independent pure-Python restatement of the same
+reference lines (Python `math` is glibc libm, like the reference build) — bit for bit.
+GPU: the kernels' own device functions (shud_physics.h through libshud_kat.so) against oracle_kat — bit for
+bit wherever only IEEE-exact operations are involved (+,-,*,/,sqrt), within the parity tolerance
+(|d| <= 1e-12|ref| + 1e-15) where OCML pow/cbrt/cos meet glibc (MANNING: cbrt; SATK: pow; SMS: cos) — a 1-ulp
+libm difference is amplified by cancellation in -1 + pow(..) and 1 - cos(..)."""
+import ctypes as C
+import math
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ATOL, ORACLE_DIR, PKG_DIR, RTOL
+from kat_grids import KAT, grid
+
+ZERO, EPSILON, EPS_SLOPE, PI, GRAV = 1e-10, 0.005, 0.05e-6, 3.1415926, 9.8
+_LIBM = C.CDLL("libm.so.6")                 # glibc cbrt (Python 3.10's math has none; numpy's is not glibc)
+_LIBM.cbrt.restype = C.c_double
+_LIBM.cbrt.argtypes = [C.c_double]
+
+
+def _oracle_lib():
+    lib = C.CDLL(os.path.join(ORACLE_DIR, "liboracle.so"))
+    lib.oracle_kat.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_void_p]
+    lib.oracle_kat.restype = C.c_int
+    return lib
+
+
+def oracle_kat(name, x):
+    out = np.zeros(x.shape[0])
+    assert _oracle_lib().oracle_kat(KAT[name], x.ctypes.data, x.shape[0], out.ctypes.data) == 0
+    return out
+
+
+# ---- pure-Python restatement (reference file:line per function) ----
+def rmin(a, b):
+    return b if a > b else a
+
+
+def rmax(a, b):
+    return b if a < b else a
+
+
+def py_manning(A, n, R, S):               # Equations.hpp:54-63, pow23 :36-39
+    t = _LIBM.cbrt(R)
+    p23 = t * t
+    if S > 0:
+        return math.sqrt(S) * A * p23 / n
+    return -1.0 * math.sqrt(-S) * A * p23 / n
+
+
+def py_effkh(ygw, aq, md, kmac, af, kmx):  # Equations.cpp:116-134
+    if md <= ZERO or ygw < aq - md:
+        return kmx
+    if ygw > aq:
+        return (kmac * md * af + kmx * (aq - md * af)) / aq
+    return (kmac * (ygw - (aq - md)) * af + kmx * (aq - md + (ygw - (aq - md)) * (1 - af))) / ygw
+
+
+def py_weir(zi, yi, zj, yj, zbank, cwr, width, thr):   # MD_RiverFlux.cpp:65-98
+    hi, hj = yi + zi, yj + zj
+    dh = hj - hi
+    if dh > 0:
+        y = hi - zbank
+        if y > 0 and yj > thr:
+            if hi > zbank:
+                y = dh
+            return cwr * math.sqrt(2. * GRAV * y) * width * y * 60.
+        return 0.
+    y = hi - zbank
+    if y > 0 and yi > thr:
+        if hj > zbank:
+            y = -dh
+        return -1. * cwr * math.sqrt(2. * GRAV * y) * width * y * 60.
+    return 0.
+
+
+def py_r2e(yr, zr, ye, ze, ke, kr, L, D):  # Flux_RiverElement.cpp:11-55
+    if ke < ZERO or kr < ZERO:
+        return 0.
+    K = (ke * 1. + kr * 1.) / (1. + 1.)
+    he, hr = ye + ze, yr + zr
+    dh = hr - he
+    if dh > ZERO:
+        A = (yr + (he - zr)) * .5 * L if he > zr else yr * L
+        return 0. if yr < EPSILON else A * K * (dh / D)
+    if dh < -ZERO:
+        if ye > ZERO:
+            return (yr + (he - zr)) * .5 * L * K * (dh / D)
+        return 0.
+    return 0.
+
+
+def py_satk(s, n):                          # Equations.cpp:136-141
+    t = -1. + math.pow(1. - math.pow(s, n / (n - 1.)), (n - 1.) / n)
+    return math.sqrt(s) * t * t
+
+
+def py_sms(ths, thr, s):                    # is_sm_et.cpp:131-140
+    fc = ths * 0.75
+    b = (s * (ths - thr) - thr) / (fc - thr)
+    b = rmin(rmax(0., b), 1.)
+    return 0.5 * (1 - math.cos(PI * b))
+
+
+def py_dady(dA, w, s):                      # functions.hpp:125-153
+    if dA == 0.:
+        return 0.
+    if abs(s) < EPS_SLOPE:
+        return dA / w
+    s = abs(s)
+    cc = w * w + 4 * s * dA
+    return -1. * w / (2. * s) if cc < ZERO else (-w + math.sqrt(cc)) / (2 * s)
+
+
+def _fix(x):
+    return 0. if x < 0. else x
+
+
+def py_geom(kind):                          # River.hpp:115-127, River.cpp:49-62
+    def f(w0, s, L, y):
+        if kind == "AREA":
+            return _fix(y * (w0 + y * s))
+        if kind == "PEREM":
+            return _fix(2.0 * math.sqrt(y * y + (y * s) * (y * s)) + w0)
+        if kind == "TOPW":
+            return _fix(y * s * 2.0 + w0)
+        return _fix(0.5 * ((y * s * 2.0 + w0) + w0) * L)
+    return f
+
+
+PY = dict(MANNING=py_manning, EFFKH=py_effkh, WEIR=py_weir, R2E=py_r2e, SATK=py_satk, SMS=py_sms, DADY=py_dady,
+          AREA=py_geom("AREA"), PEREM=py_geom("PEREM"), TOPW=py_geom("TOPW"), TOPAREA=py_geom("TOPAREA"))
+TRANSCENDENTAL = {"MANNING", "SATK", "SMS"}
+
+
+def _same(a, b):
+    return (a == b) | (np.isnan(a) & np.isnan(b))
+
+
+@pytest.mark.parametrize("name", list(KAT))
+def test_oracle_leaf_kat_vs_python(name):
+    x = grid(name)
+    got = oracle_kat(name, x)
+    want = np.array([PY[name](*row) for row in x])
+    bad = ~_same(got, want) | (np.signbit(got) != np.signbit(want))
+    assert not bad.any(), f"{name}: {bad.sum()} of {x.shape[0]} differ, first row {x[np.argmax(bad)]}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(KAT))
+def test_device_leaf_kat_vs_oracle(name):
+    lib = C.CDLL(os.path.join(PKG_DIR, "libshud_kat.so"))
+    lib.shud_kat_eval.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_void_p]
+    lib.shud_kat_eval.restype = C.c_int
+    x = grid(name)
+    got = np.zeros(x.shape[0])
+    assert lib.shud_kat_eval(KAT[name], x.ctypes.data, x.shape[0], got.ctypes.data) == 0
+    want = oracle_kat(name, x)
+    if name in TRANSCENDENTAL:     # OCML vs glibc ulps, amplified by the formulas' own cancellation
+        ok = _same(got, want) | (np.abs(got - want) <= RTOL * np.abs(want) + ATOL)
+    else:
+        ok = _same(got, want) & (np.signbit(got) == np.signbit(want))
+    assert ok.all(), f"{name}: {(~ok).sum()} of {x.shape[0]} differ, first row {x[np.argmax(~ok)]}"
