@@ -51,6 +51,9 @@ extern "C" {
 #define SHUD_EF_ET_NEG       0x04u  /* CheckNonNegative(Es..Tg)    MD_ET.cpp:394-398          [10] */
 #define SHUD_EF_ET_NAN       0x08u  /* CheckNANi(qEleETA..)        MD_ET.cpp:399-401          [10] */
 #define SHUD_EF_AET_WARN     0x10u  /* printf warning AET > 2 PET   MD_ET.cpp:391-393 (not fatal)  */
+/* ET-step prelude (include/shud_et.h, shud_et_step) */
+#define SHUD_EF_ET_RA        0x20u  /* CheckNonZero(Aerodynamic Resistance) MD_ET.cpp:273     [10] */
+#define SHUD_EF_ET_PT_NAN    0x40u  /* CheckNANi(qPotTran)          MD_ET.cpp:278              [10] */
 
 /* Static mesh description (uploaded once by shud_rhs_create).  Mirrors the derived geometry the
  * reference holds after Model_Data::initialize() (MD_initialize.cpp:168-245). */

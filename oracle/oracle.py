@@ -42,6 +42,15 @@ def lib():
         for n in ["oracle_num_calls", "oracle_num_warn"]:
             getattr(L, n).restype = C.c_longlong
             getattr(L, n).argtypes = [C.c_void_p]
+        L.oracle_et_create.restype = C.c_void_p
+        L.oracle_et_create.argtypes = [C.POINTER(abi.ShudEtMeshSoA), C.POINTER(abi.ShudEtParams)]
+        L.oracle_et_set_state.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.oracle_et_step.restype = C.c_int
+        L.oracle_et_step.argtypes = [C.c_void_p, C.POINTER(abi.ShudEtForcing)]
+        L.oracle_et_exit_index.restype = C.c_int
+        L.oracle_et_exit_index.argtypes = [C.c_void_p]
+        L.oracle_et_get.argtypes = [C.c_void_p, C.POINTER(abi.ShudEtOut)]
+        L.oracle_et_destroy.argtypes = [C.c_void_p]
         _LIB = L
     return _LIB
 
@@ -96,3 +105,44 @@ class OracleRhs:
             setattr(o, name, out[name].ctypes.data_as(abi.c_double_p))
         lib().oracle_get_diag(self.h, C.byref(o))
         return out
+
+
+class OracleEt:
+    """CPU restatement of the ET-step prelude (shud_oracle_et.c): same calls as RhsHandle.et_*."""
+
+    def __init__(self, etm):
+        self.n = etm.num_ele
+        self._m = etm.mesh_struct()
+        self._p = etm.params_struct()
+        self.h = lib().oracle_et_create(C.byref(self._m), C.byref(self._p))
+
+    def set_state(self, y_is=None, y_snow=None):
+        a = None if y_is is None else np.ascontiguousarray(y_is, dtype=np.float64)
+        b = None if y_snow is None else np.ascontiguousarray(y_snow, dtype=np.float64)
+        lib().oracle_et_set_state(self.h, None if a is None else a.ctypes.data, None if b is None else b.ctypes.data)
+
+    def step(self, forcing):
+        """returns (exit code, first element index)"""
+        fs = forcing.struct()
+        code = lib().oracle_et_step(self.h, C.byref(fs))
+        return code, lib().oracle_et_exit_index(self.h)
+
+    def get(self):
+        from shud_rhs.et import out_struct
+        o, arrs = out_struct(self.n)
+        lib().oracle_et_get(self.h, C.byref(o))
+        return arrs
+
+    def step_inputs(self):
+        """the RHS step inputs this step produced (ShudStepInputs names)"""
+        g = self.get()
+        return dict(net_prep=g["qEleNetPrep"], pot_evap=g["qPotEvap"], pot_tran=g["qPotTran"], etp=g["qEleETP"],
+                    lai=g["t_lai"], fu_surf=g["fu_surf"], fu_sub=g["fu_sub"], e_ic=g["qEleE_IC"])
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().oracle_et_destroy(self.h)
+                self.h = None
+        except Exception:  # noqa: BLE001
+            pass

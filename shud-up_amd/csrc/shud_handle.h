@@ -1,0 +1,114 @@
+// shud_handle.h — internal: the shud_rhs handle shared by the host runtime translation units
+// (shud_rhs.cpp: RHS; shud_et.cpp: ET-step prelude).  Not part of the C-ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "shud_dev.h"
+#include "shud_rhs.h"
+
+// records the message for shud_rhs_last_error_string() and returns code
+int shud_fail(int code, const char *fmt, ...);
+
+
+#define HIP_TRY(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return shud_fail(SHUD_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                        __FILE__, __LINE__);                                               \
+    } while (0)
+#define NCCL_TRY(expr)                                                                      \
+    do {                                                                                    \
+        ncclResult_t r_ = (expr);                                                           \
+        if (r_ != ncclSuccess)                                                              \
+            return shud_fail(SHUD_ERR_NCCL, "%s failed: %s", #expr, ncclGetErrorString(r_));     \
+    } while (0)
+
+
+using namespace shud;
+struct EtState;                           // shud_et.cpp
+
+struct shud_rhs {
+    int NE = 0, NR = 0, NS = 0;          // local totals (incl. ghosts)
+    int n_own = 0, n_segghost = 0, n_own_riv = 0;
+    int n_int = 0;                       // partitioned: owned prefix independent of ghost data
+    int mode = SHUD_MODE_SERIAL;
+    bool open = false;
+    bool check_errors = true;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    std::vector<void *> allocs;
+
+    DevMesh dm{};
+    DevDiag dd{};
+    bool have_diag = false;
+    int cur = 0, cur_e = 0;
+    long long ncalls = 0;
+    int variant = 0;                     // element-kernel build variant (SHUD_RHS_ELE_VARIANT, A/B only)
+    bool packed = false;                 // class-table / 16-byte-record layout in use (DevPacked)
+    DevPacked dp{};
+    int n_classes = 0;
+    bool fu_unit[2] = {true, true};      // fu_Surf / fu_Sub are all 1.0 (cryosphere off): not read
+
+    // host-pointer eval staging
+    double *d_y = nullptr, *d_ydot = nullptr, *d_scratch_dy = nullptr;
+    // replay info of the last eval
+    bool have_last = false;
+    const double *last_y = nullptr;
+    int last_cur = 0, last_cur_e = 0;
+
+    std::vector<int> seg_perm;           // element-sorted position -> reference segment index
+    int max_col[4] = {0, 0, 0, 0};       // highest BC column referenced: eyBC, eqBC, ryBC, rqBC
+    double *d_tab[4] = {nullptr, nullptr, nullptr, nullptr};
+    int tab_len[4] = {0, 0, 0, 0};
+
+    EtState *et = nullptr;               // ET-step prelude (shud_et_attach), owned
+
+    DevErr *d_err = nullptr;
+    DevErr *h_err = nullptr;             // pinned
+
+    // partition / halo
+    bool partitioned = false;
+    int rank = 0, nranks = 1;
+    bool use_nccl = false;
+    ncclComm_t comm = nullptr;
+    hipStream_t s_comm = nullptr;        // RCCL halo exchange, overlapped with the interior element kernel
+    hipEvent_t ev_pack = nullptr, ev_comm = nullptr;
+    std::vector<int> esend_off, erecv_off, rsend_off, rrecv_off;
+    int *d_esend_idx = nullptr, *d_rsend_idx = nullptr;
+    int n_esend = 0, n_rsend = 0, n_eghost = 0, n_rghost = 0;
+    double *d_esend = nullptr, *d_rsend = nullptr, *d_gele = nullptr, *d_griv = nullptr;
+
+    template <class T>
+    int dalloc(T **p, size_t n) {
+        void *q = nullptr;
+        size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+        hipError_t e = hipMalloc(&q, bytes);
+        if (e != hipSuccess) return shud_fail(SHUD_ERR_HIP, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+        allocs.push_back(q);
+        *p = (T *)q;
+        return 0;
+    }
+    template <class T>
+    int upload(T **p, const T *src, size_t n) {
+        int rc = dalloc(p, n);
+        if (rc) return rc;
+        if (n && src) HIP_TRY(hipMemcpy(*p, src, n * sizeof(T), hipMemcpyHostToDevice));
+        else if (n) HIP_TRY(hipMemset(*p, 0, n * sizeof(T)));
+        return 0;
+    }
+    template <class T>
+    int upload_fill(T **p, const T *src, size_t n, T fill) {
+        if (src) return upload(p, src, n);
+        std::vector<T> tmp(n, fill);
+        return upload(p, tmp.data(), n);
+    }
+};
+
+int shud_reset_err(shud_rhs *h);
+void shud_et_free(shud_rhs *h);          // shud_et.cpp

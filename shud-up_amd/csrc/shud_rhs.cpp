@@ -23,16 +23,15 @@
 #include <unordered_map>
 #include <vector>
 
-#include "shud_dev.h"
-#include "shud_rhs.h"
+#include "shud_handle.h"
 
 using namespace shud;
 
 namespace {
-
 thread_local std::string g_last_error;
+}  // namespace
 
-int fail(int code, const char *fmt, ...) {
+int shud_fail(int code, const char *fmt, ...) {
     char buf[512];
     va_list ap;
     va_start(ap, fmt);
@@ -42,99 +41,7 @@ int fail(int code, const char *fmt, ...) {
     return code;
 }
 
-#define HIP_TRY(expr)                                                                      \
-    do {                                                                                   \
-        hipError_t e_ = (expr);                                                            \
-        if (e_ != hipSuccess)                                                              \
-            return fail(SHUD_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
-                        __FILE__, __LINE__);                                               \
-    } while (0)
-#define NCCL_TRY(expr)                                                                      \
-    do {                                                                                    \
-        ncclResult_t r_ = (expr);                                                           \
-        if (r_ != ncclSuccess)                                                              \
-            return fail(SHUD_ERR_NCCL, "%s failed: %s", #expr, ncclGetErrorString(r_));     \
-    } while (0)
-
-}  // namespace
-
-struct shud_rhs {
-    int NE = 0, NR = 0, NS = 0;          // local totals (incl. ghosts)
-    int n_own = 0, n_segghost = 0, n_own_riv = 0;
-    int n_int = 0;                       // partitioned: owned prefix independent of ghost data
-    int mode = SHUD_MODE_SERIAL;
-    bool open = false;
-    bool check_errors = true;
-    int device = 0;
-    hipStream_t stream = nullptr;
-    bool own_stream = false;
-    std::vector<void *> allocs;
-
-    DevMesh dm{};
-    DevDiag dd{};
-    bool have_diag = false;
-    int cur = 0, cur_e = 0;
-    long long ncalls = 0;
-    int variant = 0;                     // element-kernel build variant (SHUD_RHS_ELE_VARIANT, A/B only)
-    bool packed = false;                 // class-table / 16-byte-record layout in use (DevPacked)
-    DevPacked dp{};
-    int n_classes = 0;
-    bool fu_unit[2] = {true, true};      // fu_Surf / fu_Sub are all 1.0 (cryosphere off): not read
-
-    // host-pointer eval staging
-    double *d_y = nullptr, *d_ydot = nullptr, *d_scratch_dy = nullptr;
-    // replay info of the last eval
-    bool have_last = false;
-    const double *last_y = nullptr;
-    int last_cur = 0, last_cur_e = 0;
-
-    std::vector<int> seg_perm;           // element-sorted position -> reference segment index
-    int max_col[4] = {0, 0, 0, 0};       // highest BC column referenced: eyBC, eqBC, ryBC, rqBC
-    double *d_tab[4] = {nullptr, nullptr, nullptr, nullptr};
-    int tab_len[4] = {0, 0, 0, 0};
-
-    DevErr *d_err = nullptr;
-    DevErr *h_err = nullptr;             // pinned
-
-    // partition / halo
-    bool partitioned = false;
-    int rank = 0, nranks = 1;
-    bool use_nccl = false;
-    ncclComm_t comm = nullptr;
-    hipStream_t s_comm = nullptr;        // RCCL halo exchange, overlapped with the interior element kernel
-    hipEvent_t ev_pack = nullptr, ev_comm = nullptr;
-    std::vector<int> esend_off, erecv_off, rsend_off, rrecv_off;
-    int *d_esend_idx = nullptr, *d_rsend_idx = nullptr;
-    int n_esend = 0, n_rsend = 0, n_eghost = 0, n_rghost = 0;
-    double *d_esend = nullptr, *d_rsend = nullptr, *d_gele = nullptr, *d_griv = nullptr;
-
-    template <class T>
-    int dalloc(T **p, size_t n) {
-        void *q = nullptr;
-        size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
-        hipError_t e = hipMalloc(&q, bytes);
-        if (e != hipSuccess) return fail(SHUD_ERR_HIP, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
-        allocs.push_back(q);
-        *p = (T *)q;
-        return 0;
-    }
-    template <class T>
-    int upload(T **p, const T *src, size_t n) {
-        int rc = dalloc(p, n);
-        if (rc) return rc;
-        if (n && src) HIP_TRY(hipMemcpy(*p, src, n * sizeof(T), hipMemcpyHostToDevice));
-        else if (n) HIP_TRY(hipMemset(*p, 0, n * sizeof(T)));
-        return 0;
-    }
-    template <class T>
-    int upload_fill(T **p, const T *src, size_t n, T fill) {
-        if (src) return upload(p, src, n);
-        std::vector<T> tmp(n, fill);
-        return upload(p, tmp.data(), n);
-    }
-};
-
-static int reset_err(shud_rhs *h) {
+int shud_reset_err(shud_rhs *h) {
     DevErr z{};
     z.flags = 0;
     for (int k = 0; k < 8; k++) z.first_index[k] = INT_MAX;
@@ -157,10 +64,10 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
 static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, const ShudRhsOptions *opt,
                  const ShudPartition *part) {
     const int NE = m->num_ele, NR = m->num_riv, NS = m->num_seg;
-    if (NE < 0 || NR < 0 || NS < 0) return fail(SHUD_ERR_ARG, "negative sizes");
+    if (NE < 0 || NR < 0 || NS < 0) return shud_fail(SHUD_ERR_ARG, "negative sizes");
     h->NE = NE; h->NR = NR; h->NS = NS;
     h->mode = opt ? opt->mode : SHUD_MODE_SERIAL;
-    if (h->mode != SHUD_MODE_SERIAL && h->mode != SHUD_MODE_OMP) return fail(SHUD_ERR_ARG, "bad mode %d", h->mode);
+    if (h->mode != SHUD_MODE_SERIAL && h->mode != SHUD_MODE_OMP) return shud_fail(SHUD_ERR_ARG, "bad mode %d", h->mode);
     h->check_errors = opt ? opt->check_errors != 0 : true;
     h->open = (m->close_boundary == 0);
     h->device = opt ? opt->device : 0;
@@ -169,40 +76,40 @@ static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, cons
     h->n_own_riv = part ? part->n_own_riv : NR;
     if (const char *v = getenv("SHUD_RHS_ELE_VARIANT")) h->variant = atoi(v);
     if (h->n_own < 0 || h->n_own + h->n_segghost > NE || h->n_own_riv < 0 || h->n_own_riv > NR)
-        return fail(SHUD_ERR_ARG, "partition counts inconsistent with mesh sizes");
+        return shud_fail(SHUD_ERR_ARG, "partition counts inconsistent with mesh sizes");
 
     // ---- validation (the reference exits on these at run time; we reject them up front) ----
     if (!m->nabr || !m->area || !m->z_surf || !m->z_bottom || !m->edge || !m->dist2nabor || !m->avg_rough)
-        return fail(SHUD_ERR_ARG, "missing element geometry array");
-    if (h->open && (!m->dist2edge || !m->rough)) return fail(SHUD_ERR_ARG, "open boundary needs dist2edge and rough");
+        return shud_fail(SHUD_ERR_ARG, "missing element geometry array");
+    if (h->open && (!m->dist2edge || !m->rough)) return shud_fail(SHUD_ERR_ARG, "open boundary needs dist2edge and rough");
     if (NR && (!m->riv_down || !m->riv_length || !m->riv_bed_slope || !m->riv_dist2down || !m->riv_avg_rough ||
                !m->riv_depth || !m->riv_bottom_width || !m->riv_bankslope || !m->riv_ksath || !m->riv_bedthick))
-        return fail(SHUD_ERR_ARG, "missing river array");
-    if (NS && (!m->seg_ele || !m->seg_riv || !m->seg_length || !m->seg_cwr)) return fail(SHUD_ERR_ARG, "missing segment array");
+        return shud_fail(SHUD_ERR_ARG, "missing river array");
+    if (NS && (!m->seg_ele || !m->seg_riv || !m->seg_length || !m->seg_cwr)) return shud_fail(SHUD_ERR_ARG, "missing segment array");
     const double *pp[17] = {p->aquifer_depth, p->macD, p->macKsatH, p->geo_vAreaF, p->KsatH, p->KsatV,
                             p->infKsatV, p->hAreaF, p->macKsatV, p->ThetaS, p->ThetaR, p->Beta,
                             p->infD, p->Sy, p->RzD, p->VegFrac, p->ImpAF};
     for (int k = 0; k < 17; k++)
-        if (!pp[k]) return fail(SHUD_ERR_ARG, "missing parameter array #%d", k);
+        if (!pp[k]) return shud_fail(SHUD_ERR_ARG, "missing parameter array #%d", k);
     for (long long q = 0; q < 3LL * NE; q++)
-        if (m->nabr[q] < -1 || m->nabr[q] >= NE) return fail(SHUD_ERR_ARG, "nabr[%lld]=%d out of range", q, m->nabr[q]);
+        if (m->nabr[q] < -1 || m->nabr[q] >= NE) return shud_fail(SHUD_ERR_ARG, "nabr[%lld]=%d out of range", q, m->nabr[q]);
     if (m->ilake)
         for (int i = 0; i < NE; i++)
-            if (m->ilake[i] > 0) return fail(SHUD_ERR_UNSUPPORTED, "lake element %d: lake module not supported", i);
+            if (m->ilake[i] > 0) return shud_fail(SHUD_ERR_UNSUPPORTED, "lake element %d: lake module not supported", i);
     for (int r = 0; r < NR; r++) {
         int d = m->riv_down[r];
         if (d >= NR || (d < 0 && d < -4))
-            return fail(SHUD_ERR_ARG, "Fatal Error: River Routing Boundary Condition Type Is Wrong! (reach %d down %d)", r, d);
+            return shud_fail(SHUD_ERR_ARG, "Fatal Error: River Routing Boundary Condition Type Is Wrong! (reach %d down %d)", r, d);
     }
     for (int s = 0; s < NS; s++)
         if (m->seg_ele[s] < 0 || m->seg_ele[s] >= NE || m->seg_riv[s] < 0 || m->seg_riv[s] >= NR)
-            return fail(SHUD_ERR_ARG, "segment %d references element/reach out of range", s);
+            return shud_fail(SHUD_ERR_ARG, "segment %d references element/reach out of range", s);
 
     // ---- packed element flags, BC column maxima ----
     std::vector<int> eflags(NE);
     for (int i = 0; i < NE; i++) {
         int ibc = m->ibc ? m->ibc[i] : 0, iss = m->iss ? m->iss[i] : 0;
-        if (ibc < -32768 || ibc > 32767) return fail(SHUD_ERR_ARG, "iBC out of range at %d", i);
+        if (ibc < -32768 || ibc > 32767) return shud_fail(SHUD_ERR_ARG, "iBC out of range at %d", i);
         eflags[i] = (ibc & 0xffff) | ((iss > 0 ? 1 : iss < 0 ? 2 : 0) << 16);
         if (ibc > 0) h->max_col[0] = std::max(h->max_col[0], ibc);
         if (ibc < 0) h->max_col[1] = std::max(h->max_col[1], -ibc);
@@ -233,7 +140,7 @@ static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, cons
     // only elements < ncomp compute their segments; segments of pure ghosts must not be needed
     for (int s = 0; s < NS; s++)
         if (m->seg_ele[s] >= ncomp && m->seg_riv[s] < h->n_own_riv)
-            return fail(SHUD_ERR_ARG, "segment %d of an owned reach belongs to a non-computed ghost element", s);
+            return shud_fail(SHUD_ERR_ARG, "segment %d of an owned reach belongs to a non-computed ghost element", s);
     h->seg_perm = order;
     // ---- partitioned: owned elements [0, n_int) read no ghost data (all lateral neighbours owned, all their
     // segments' reaches owned); they run while the halo exchange is in flight (eval_device) ----
@@ -363,7 +270,7 @@ static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, cons
     if ((rc = h->dalloc(&h->d_err, 1))) return rc;
     d.err = h->d_err;
     HIP_TRY(hipHostMalloc((void **)&h->h_err, sizeof(DevErr), hipHostMallocDefault));
-    if ((rc = reset_err(h))) return rc;
+    if ((rc = shud_reset_err(h))) return rc;
     const size_t ny = 3 * (size_t)h->n_own + h->n_own_riv;
     if ((rc = h->dalloc(&h->d_y, ny))) return rc;
     if ((rc = h->dalloc(&h->d_ydot, ny))) return rc;
@@ -540,7 +447,7 @@ static int setup_partition(shud_rhs *h, const ShudPartition *part) {
     h->rank = part->rank;
     h->nranks = part->nranks;
     const int P = part->nranks;
-    if (P < 1 || part->rank < 0 || part->rank >= P) return fail(SHUD_ERR_ARG, "bad rank/nranks");
+    if (P < 1 || part->rank < 0 || part->rank >= P) return shud_fail(SHUD_ERR_ARG, "bad rank/nranks");
     h->esend_off.assign(part->ele_send_off, part->ele_send_off + P + 1);
     h->erecv_off.assign(part->ele_recv_off, part->ele_recv_off + P + 1);
     h->rsend_off.assign(part->riv_send_off, part->riv_send_off + P + 1);
@@ -549,12 +456,12 @@ static int setup_partition(shud_rhs *h, const ShudPartition *part) {
     h->n_rsend = h->rsend_off[P];
     h->n_eghost = h->erecv_off[P];
     h->n_rghost = h->rrecv_off[P];
-    if (h->n_own + h->n_eghost != h->NE) return fail(SHUD_ERR_ARG, "ghost element count mismatch");
-    if (h->n_own_riv + h->n_rghost != h->NR) return fail(SHUD_ERR_ARG, "ghost reach count mismatch");
+    if (h->n_own + h->n_eghost != h->NE) return shud_fail(SHUD_ERR_ARG, "ghost element count mismatch");
+    if (h->n_own_riv + h->n_rghost != h->NR) return shud_fail(SHUD_ERR_ARG, "ghost reach count mismatch");
     for (int k = 0; k < h->n_esend; k++)
-        if (part->ele_send_idx[k] < 0 || part->ele_send_idx[k] >= h->n_own) return fail(SHUD_ERR_ARG, "bad ele_send_idx");
+        if (part->ele_send_idx[k] < 0 || part->ele_send_idx[k] >= h->n_own) return shud_fail(SHUD_ERR_ARG, "bad ele_send_idx");
     for (int k = 0; k < h->n_rsend; k++)
-        if (part->riv_send_idx[k] < 0 || part->riv_send_idx[k] >= h->n_own_riv) return fail(SHUD_ERR_ARG, "bad riv_send_idx");
+        if (part->riv_send_idx[k] < 0 || part->riv_send_idx[k] >= h->n_own_riv) return shud_fail(SHUD_ERR_ARG, "bad riv_send_idx");
     int rc;
     if ((rc = h->upload(&h->d_esend_idx, part->ele_send_idx, h->n_esend))) return rc;
     if ((rc = h->upload(&h->d_rsend_idx, part->riv_send_idx, h->n_rsend))) return rc;
@@ -580,6 +487,7 @@ static void destroy_handle(shud_rhs *h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->s_comm) (void)hipStreamSynchronize(h->s_comm);
     if (h->comm) ncclCommDestroy(h->comm);
+    shud_et_free(h);
     if (h->ev_pack) (void)hipEventDestroy(h->ev_pack);
     if (h->ev_comm) (void)hipEventDestroy(h->ev_comm);
     if (h->s_comm) (void)hipStreamDestroy(h->s_comm);
@@ -591,7 +499,7 @@ static void destroy_handle(shud_rhs *h) {
 
 extern "C" int shud_rhs_create(const ShudMeshSoA *mesh, const ShudParamsSoA *par, const ShudRhsOptions *opt,
                                shud_rhs_t *out) {
-    if (!mesh || !par || !out) return fail(SHUD_ERR_ARG, "null argument");
+    if (!mesh || !par || !out) return shud_fail(SHUD_ERR_ARG, "null argument");
     shud_rhs *h = new shud_rhs();
     int rc = build(h, mesh, par, opt, nullptr);
     if (rc) { destroy_handle(h); return rc; }
@@ -610,7 +518,7 @@ extern "C" int shud_rhs_nccl_unique_id(char out[128]) {
 extern "C" int shud_rhs_create_partitioned(const ShudMeshSoA *mesh, const ShudParamsSoA *par,
                                            const ShudRhsOptions *opt, const ShudPartition *part,
                                            shud_rhs_t *out) {
-    if (!mesh || !par || !part || !out) return fail(SHUD_ERR_ARG, "null argument");
+    if (!mesh || !par || !part || !out) return shud_fail(SHUD_ERR_ARG, "null argument");
     shud_rhs *h = new shud_rhs();
     int rc = build(h, mesh, par, opt, part);
     if (!rc) rc = setup_partition(h, part);
@@ -628,7 +536,7 @@ extern "C" int shud_rhs_destroy(shud_rhs_t h) {
 // step inputs
 // ---------------------------------------------------------------------------------------------
 extern "C" int shud_rhs_set_step_inputs(shud_rhs_t h, const ShudStepInputs *in) {
-    if (!h || !in) return fail(SHUD_ERR_ARG, "null argument");
+    if (!h || !in) return shud_fail(SHUD_ERR_ARG, "null argument");
     HIP_TRY(hipSetDevice(h->device));
     const size_t nb = (size_t)h->NE * sizeof(double);
     // packed layout: carried-state overrides go through SoA staging slot 0, then into the packed record
@@ -662,7 +570,7 @@ extern "C" int shud_rhs_set_step_inputs(shud_rhs_t h, const ShudStepInputs *in) 
     for (int k = 0; k < 4; k++) {
         if (!tabs[k]) continue;
         if (ns[k] < h->max_col[k])
-            return fail(SHUD_ERR_ARG, "BC table %d has %d columns, mesh references column %d", k, ns[k], h->max_col[k]);
+            return shud_fail(SHUD_ERR_ARG, "BC table %d has %d columns, mesh references column %d", k, ns[k], h->max_col[k]);
         HIP_TRY(hipMemcpyAsync(h->d_tab[k], tabs[k], (size_t)h->tab_len[k] * sizeof(double), hipMemcpyHostToDevice,
                                h->stream));
     }
@@ -766,10 +674,10 @@ static int eval_device(shud_rhs *h, double t, const double *y, double *dy) {
 }
 
 extern "C" int shud_rhs_eval(shud_rhs_t h, double t, const double *y, double *ydot, int where) {
-    if (!h || !y || !ydot) return fail(SHUD_ERR_ARG, "null argument");
+    if (!h || !y || !ydot) return shud_fail(SHUD_ERR_ARG, "null argument");
     const size_t ny = 3 * (size_t)h->n_own + h->n_own_riv;
     if (where == SHUD_WHERE_DEVICE) return eval_device(h, t, y, ydot);
-    if (where != SHUD_WHERE_HOST) return fail(SHUD_ERR_ARG, "bad where");
+    if (where != SHUD_WHERE_HOST) return shud_fail(SHUD_ERR_ARG, "bad where");
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(hipMemcpyAsync(h->d_y, y, ny * sizeof(double), hipMemcpyHostToDevice, h->stream));
     int rc = eval_device(h, t, h->d_y, h->d_ydot);
@@ -777,7 +685,7 @@ extern "C" int shud_rhs_eval(shud_rhs_t h, double t, const double *y, double *yd
     HIP_TRY(hipMemcpyAsync(ydot, h->d_ydot, ny * sizeof(double), hipMemcpyDeviceToHost, h->stream));
     if (h->check_errors) {
         if ((rc = read_err(h))) return rc;
-        if (h->h_err->flags & kFatal) return fail(SHUD_ERR_PHYSICS, "physics error flags 0x%x", h->h_err->flags);
+        if (h->h_err->flags & kFatal) return shud_fail(SHUD_ERR_PHYSICS, "physics error flags 0x%x", h->h_err->flags);
     } else {
         HIP_TRY(hipStreamSynchronize(h->stream));
     }
@@ -787,7 +695,7 @@ extern "C" int shud_rhs_eval(shud_rhs_t h, double t, const double *y, double *yd
 extern "C" long long shud_rhs_num_calls(shud_rhs_t h) { return h ? h->ncalls : -1; }
 
 extern "C" int shud_rhs_layout(shud_rhs_t h, int *packed, int *n_classes) {
-    if (!h) return fail(SHUD_ERR_ARG, "null argument");
+    if (!h) return shud_fail(SHUD_ERR_ARG, "null argument");
     if (packed) *packed = h->packed ? 1 : 0;
     if (n_classes) *n_classes = h->n_classes;
     return SHUD_OK;
@@ -797,7 +705,7 @@ extern "C" int shud_rhs_layout(shud_rhs_t h, int *packed, int *n_classes) {
 // errors
 // ---------------------------------------------------------------------------------------------
 extern "C" int shud_rhs_get_error(shud_rhs_t h, ShudErr *e) {
-    if (!h || !e) return fail(SHUD_ERR_ARG, "null argument");
+    if (!h || !e) return shud_fail(SHUD_ERR_ARG, "null argument");
     HIP_TRY(hipSetDevice(h->device));
     int rc = read_err(h);
     if (rc) return rc;
@@ -806,6 +714,18 @@ extern "C" int shud_rhs_get_error(shud_rhs_t h, ShudErr *e) {
     e->flags = d.flags;
     for (int k = 0; k < 8; k++) e->first_index[k] = (d.first_index[k] == INT_MAX) ? -1 : d.first_index[k];
     e->n_aet_warn = (int64_t)d.n_warn;
+    // ET-step prelude (shud_et_step): tReadForcing's CheckNonZero(ra) then CheckNANi(qPotTran), per element
+    if (d.flags & (SHUD_EF_ET_RA | SHUD_EF_ET_PT_NAN)) {
+        const int ra = (d.flags & SHUD_EF_ET_RA) ? d.first_index[5] : INT_MAX;
+        const int pt = (d.flags & SHUD_EF_ET_PT_NAN) ? d.first_index[6] : INT_MAX;
+        e->exit_code = 10;
+        if (ra <= pt)
+            snprintf(e->message, sizeof(e->message),
+                     "ERROR: Value for Aerodynamic Resistance of Element %d is not allowed. Please check again.", ra + 1);
+        else
+            snprintf(e->message, sizeof(e->message), "ERROR: NAN error for qPotTran[i] %d", pt + 1);
+        return SHUD_OK;
+    }
     // the reference stops at the first myexit() in loop order: loop A (f_etFlux then effKH, per element,
     // MD_f.cpp:11-26), then the applyDY NaN check (MD_f.cpp:73-74)
     int et = INT_MAX;
@@ -830,8 +750,8 @@ extern "C" int shud_rhs_get_error(shud_rhs_t h, ShudErr *e) {
 }
 
 extern "C" int shud_rhs_clear_error(shud_rhs_t h) {
-    if (!h) return fail(SHUD_ERR_ARG, "null argument");
-    return reset_err(h);
+    if (!h) return shud_fail(SHUD_ERR_ARG, "null argument");
+    return shud_reset_err(h);
 }
 
 extern "C" int shud_rhs_cvrhs(double t, const double *y, double *ydot, void *user_data) {
@@ -871,8 +791,8 @@ static int ensure_diag(shud_rhs *h) {
 }
 
 extern "C" int shud_rhs_sync_diagnostics(shud_rhs_t h, ShudFluxOut *o) {
-    if (!h || !o) return fail(SHUD_ERR_ARG, "null argument");
-    if (!h->have_last) return fail(SHUD_ERR_ARG, "no evaluation to report diagnostics for");
+    if (!h || !o) return shud_fail(SHUD_ERR_ARG, "null argument");
+    if (!h->have_last) return shud_fail(SHUD_ERR_ARG, "no evaluation to report diagnostics for");
     HIP_TRY(hipSetDevice(h->device));
     int rc = ensure_diag(h);
     if (rc) return rc;
@@ -925,7 +845,7 @@ extern "C" int shud_rhs_sync_diagnostics(shud_rhs_t h, ShudFluxOut *o) {
 // measurement helpers
 // ---------------------------------------------------------------------------------------------
 extern "C" int shud_rhs_device_alloc(shud_rhs_t h, size_t bytes, void **dptr) {
-    if (!h || !dptr) return fail(SHUD_ERR_ARG, "null argument");
+    if (!h || !dptr) return shud_fail(SHUD_ERR_ARG, "null argument");
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(hipMalloc(dptr, bytes ? bytes : 8));
     return SHUD_OK;
@@ -936,14 +856,14 @@ extern "C" int shud_rhs_device_free(shud_rhs_t h, void *dptr) {
     return SHUD_OK;
 }
 extern "C" int shud_rhs_memcpy(shud_rhs_t h, void *dst, const void *src, size_t bytes, int kind) {
-    if (!h) return fail(SHUD_ERR_ARG, "null argument");
+    if (!h) return shud_fail(SHUD_ERR_ARG, "null argument");
     hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : kind == 2 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
     HIP_TRY(hipMemcpyAsync(dst, src, bytes, k, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     return SHUD_OK;
 }
 extern "C" int shud_rhs_synchronize(shud_rhs_t h) {
-    if (!h) return fail(SHUD_ERR_ARG, "null argument");
+    if (!h) return shud_fail(SHUD_ERR_ARG, "null argument");
     HIP_TRY(hipStreamSynchronize(h->stream));
     return SHUD_OK;
 }
@@ -951,13 +871,13 @@ extern "C" void *shud_rhs_stream(shud_rhs_t h) { return h ? (void *)h->stream : 
 
 // halo buffers of a partitioned handle (external-transport tests move them between handles)
 extern "C" int shud_rhs_halo_buffers(shud_rhs_t h, double **esend, double **rsend, double **gele, double **griv) {
-    if (!h || !h->partitioned) return fail(SHUD_ERR_ARG, "not a partitioned handle");
+    if (!h || !h->partitioned) return shud_fail(SHUD_ERR_ARG, "not a partitioned handle");
     *esend = h->d_esend; *rsend = h->d_rsend; *gele = h->d_gele; *griv = h->d_griv;
     return SHUD_OK;
 }
 // split eval for external transport: pack, (caller exchanges), compute
 extern "C" int shud_rhs_eval_pack(shud_rhs_t h, const double *d_y) {
-    if (!h || !h->partitioned) return fail(SHUD_ERR_ARG, "not a partitioned handle");
+    if (!h || !h->partitioned) return shud_fail(SHUD_ERR_ARG, "not a partitioned handle");
     launch_pack_kernel(d_y, h->n_own, h->n_own_riv, h->d_esend_idx, h->n_esend, h->d_rsend_idx, h->n_rsend,
                        h->d_esend, h->d_rsend, h->stream);
     HIP_TRY(hipGetLastError());
@@ -965,7 +885,7 @@ extern "C" int shud_rhs_eval_pack(shud_rhs_t h, const double *d_y) {
 }
 extern "C" int shud_rhs_eval_compute(shud_rhs_t h, double t, const double *d_y, double *d_ydot) {
     (void)t;
-    if (!h) return fail(SHUD_ERR_ARG, "null argument");
+    if (!h) return shud_fail(SHUD_ERR_ARG, "null argument");
     h->last_cur = h->cur;
     h->last_cur_e = h->cur_e;
     int rc = launch_split(h, d_y, d_ydot);
@@ -980,7 +900,7 @@ extern "C" int shud_rhs_eval_compute(shud_rhs_t h, double t, const double *d_y, 
 extern "C" int shud_rhs_time_kernels(shud_rhs_t h, double t, const double *d_y, double *d_ydot, int reps,
                                      double *ms_eval, double *ms_out, int *nk, char *names_out, int names_len) {
     (void)t;
-    if (!h || reps <= 0) return fail(SHUD_ERR_ARG, "bad argument");
+    if (!h || reps <= 0) return shud_fail(SHUD_ERR_ARG, "bad argument");
     HIP_TRY(hipSetDevice(h->device));
     const int K = h->partitioned ? 3 : 2;
     std::vector<hipEvent_t> ev((size_t)reps * (K + 1));

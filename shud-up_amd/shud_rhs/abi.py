@@ -25,6 +25,9 @@ EF_EFFKH = 0x02
 EF_ET_NEG = 0x04
 EF_ET_NAN = 0x08
 EF_AET_WARN = 0x10
+EF_ET_RA = 0x20
+EF_ET_PT_NAN = 0x40
+SHUD_TSR_OFF, SHUD_TSR_NO_TIME, SHUD_TSR_CACHED, SHUD_TSR_RECOMPUTE = 0, 1, 2, 3
 
 MESH_FIELDS = [
     ("num_ele", C.c_int32), ("num_riv", C.c_int32), ("num_seg", C.c_int32), ("close_boundary", C.c_int32),
@@ -94,6 +97,41 @@ class ShudPartition(C.Structure):
                 ("ele_gid", c_int32_p), ("riv_gid", c_int32_p), ("nccl_unique_id", C.c_char_p)]
 
 
+# ---- include/shud_et.h (ET-step prelude) ----
+class ShudEtMeshSoA(C.Structure):
+    _fields_ = [("num_ele", C.c_int32), ("iforc", c_int32_p), ("ilc", c_int32_p), ("imf", c_int32_p),
+                ("z_surf", c_double_p), ("albedo", c_double_p), ("fix_pressure", c_double_p), ("wind_h", c_double_p),
+                ("veg_frac", c_double_p), ("ilake", c_int32_p), ("nx", c_double_p), ("ny", c_double_p),
+                ("nz", c_double_p)]
+
+
+ET_PARAM_D = ["cPrep", "cTemp", "cLAItsd", "cMF", "cETP", "cISmax"]
+
+
+class ShudEtParams(C.Structure):
+    _fields_ = [(n, C.c_double) for n in ET_PARAM_D] + [
+        ("radiation_input_mode", C.c_int32), ("terrain_radiation", C.c_int32), ("rad_factor_cap", C.c_double),
+        ("rad_cosz_min", C.c_double), ("cryosphere", C.c_int32), ("ft_surf_day", C.c_int32),
+        ("ft_sub_day", C.c_int32), ("ft_surf_max", C.c_double), ("ft_surf_min", C.c_double),
+        ("ft_sub_max", C.c_double), ("ft_sub_min", C.c_double)]
+
+
+class ShudEtForcing(C.Structure):
+    _fields_ = [("t", C.c_double), ("t_next", C.c_double), ("n_station", C.c_int32), ("station", c_double_p),
+                ("station_z", c_double_p), ("n_lai_col", C.c_int32), ("lai_row", c_double_p),
+                ("n_mf_col", C.c_int32), ("mf_row", c_double_p), ("tsr_mode", C.c_int32), ("tsr_n", C.c_int32),
+                ("tsr_sx", c_double_p), ("tsr_sy", c_double_p), ("tsr_sz", c_double_p), ("tsr_wdt", c_double_p),
+                ("tsr_den", C.c_double)]
+
+
+ET_OUT = ["t_prcp", "t_temp", "t_lai", "t_mf", "t_rn", "t_wind", "t_rh", "qEleprep", "qPotEvap", "qPotTran",
+          "qEleETP", "qEleNetPrep", "qEleE_IC", "yEleIS", "yEleSnow", "fu_surf", "fu_sub", "rn_factor"]
+
+
+class ShudEtOut(C.Structure):
+    _fields_ = [(n, c_double_p) for n in ET_OUT]
+
+
 # functions declared in include/shud_rhs.h (name -> (restype, argtypes))
 _H = C.c_void_p
 FUNCTIONS = {
@@ -126,10 +164,17 @@ FUNCTIONS = {
     "shud_rhs_eval_pack": (C.c_int, [_H, C.c_void_p]),
     "shud_rhs_eval_compute": (C.c_int, [_H, C.c_double, C.c_void_p, C.c_void_p]),
 }
+# include/shud_et.h
+ET_FUNCTIONS = {
+    "shud_et_attach": (C.c_int, [_H, C.POINTER(ShudEtMeshSoA), C.POINTER(ShudEtParams)]),
+    "shud_et_set_state": (C.c_int, [_H, C.c_void_p, C.c_void_p]),
+    "shud_et_step": (C.c_int, [_H, C.POINTER(ShudEtForcing)]),
+    "shud_et_get": (C.c_int, [_H, C.POINTER(ShudEtOut)]),
+}
 
 
 def bind(lib):
-    for name, (res, args) in FUNCTIONS.items():
+    for name, (res, args) in list(FUNCTIONS.items()) + list(ET_FUNCTIONS.items()):
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args

@@ -167,6 +167,34 @@ class RhsHandle:
         _check(lib().shud_rhs_halo_buffers(self.h, *[C.byref(x) for x in p]), "halo_buffers")
         return [x.value for x in p]
 
+    # ---- ET-step prelude (include/shud_et.h) ----
+    def et_attach(self, etm):
+        self._et_mesh = etm.mesh_struct()
+        self._et_par = etm.params_struct()
+        _check(lib().shud_et_attach(self.h, C.byref(self._et_mesh), C.byref(self._et_par)), "shud_et_attach")
+
+    def et_set_state(self, y_is=None, y_snow=None):
+        a = None if y_is is None else np.ascontiguousarray(y_is, dtype=np.float64)
+        b = None if y_snow is None else np.ascontiguousarray(y_snow, dtype=np.float64)
+        _check(lib().shud_et_set_state(self.h, None if a is None else a.ctypes.data,
+                                       None if b is None else b.ctypes.data), "shud_et_set_state")
+
+    def et_step(self, forcing, raise_on_physics=True):
+        fs = forcing.struct()
+        rc = lib().shud_et_step(self.h, C.byref(fs))
+        if rc == abi.SHUD_ERR_PHYSICS and raise_on_physics:
+            e = self.get_error()
+            raise ShudRhsError(rc, e["message"], e)
+        if rc not in (abi.SHUD_OK, abi.SHUD_ERR_PHYSICS):
+            _check(rc, "shud_et_step")
+        return rc
+
+    def et_get(self):
+        from .et import out_struct
+        o, arrs = out_struct(self.model.num_ele)
+        _check(lib().shud_et_get(self.h, C.byref(o)), "shud_et_get")
+        return arrs
+
     def eval_pack(self, d_y):
         _check(lib().shud_rhs_eval_pack(self.h, C.c_void_p(d_y)), "eval_pack")
 

@@ -28,19 +28,41 @@ def load_fixture(name):
     return m, y0
 
 
-def assert_close(got, ref, rtol=RTOL, atol=ATOL, what=""):
+def assert_close(got, ref, rtol=RTOL, atol=ATOL, what="", blocks=None, max_cancel=1e-3):
+    """Per entry |got - ref| <= rtol*|ref| + atol.  With `blocks` (slices of one state vector, e.g. the
+    sf/us/gw/riv blocks of DY), an entry that misses it may instead satisfy |got - ref| <= rtol*max|ref| of
+    its block: a DY that is a near-cancelling sum of much larger fluxes inherits the libm ulps (OCML vs
+    glibc) of those fluxes, not of its own size.  At most a fraction max_cancel of the entries may need
+    that allowance; they are returned in the report."""
     got = np.asarray(got)
     ref = np.asarray(ref)
     both_nan = np.isnan(got) & np.isnan(ref)
     err = np.abs(got - ref)
-    bad = ~((err <= rtol * np.abs(ref) + atol) | both_nan | (got == ref))
+    ok = (err <= rtol * np.abs(ref) + atol) | both_nan | (got == ref)
+    n_cancel = 0
+    if blocks is not None and not ok.all():
+        scale = np.zeros_like(err)
+        for b in blocks:
+            blk = np.abs(ref[b])
+            scale[b] = blk[np.isfinite(blk)].max() if np.isfinite(blk).any() else 0.0
+        cancel = ~ok & (err <= rtol * scale + atol)
+        n_cancel = int(cancel.sum())
+        if n_cancel <= max_cancel * ok.size:
+            ok |= cancel
+    bad = ~ok
     if bad.any():
         i = np.nonzero(bad)[0][:5]
         raise AssertionError(f"{what}: {bad.sum()} of {bad.size} entries outside tolerance; first {i}: "
-                             f"got {got[i]} ref {ref[i]}")
+                             f"got {got[i]} ref {ref[i]} |d| {err[i]} ({n_cancel} cancellation entries)")
     finite = np.isfinite(ref) & (ref != 0)
     rel = (err[finite] / np.abs(ref[finite])).max() if finite.any() else 0.0
     return float(err[~both_nan].max() if (~both_nan).any() else 0.0), float(rel)
+
+
+def rhs_blocks(m):
+    """the sf / us / gw / riv blocks of a DY vector of model m"""
+    ne, nr = m.num_ele, m.num_riv
+    return [slice(0, ne), slice(ne, 2 * ne), slice(2 * ne, 3 * ne), slice(3 * ne, 3 * ne + nr)]
 
 
 @pytest.fixture(scope="session")

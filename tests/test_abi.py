@@ -8,20 +8,26 @@ import subprocess
 from conftest import ROOT
 from shud_rhs import abi
 
-HEADER = os.path.join(ROOT, "include", "shud_rhs.h")
+HEADERS = {"shud_rhs.h": ("shud_rhs_", abi.FUNCTIONS), "shud_et.h": ("shud_et_", abi.ET_FUNCTIONS)}
 LIB = os.path.join(ROOT, "shud-up_amd", "libshud_rhs.so")
 
 
-def header_functions():
-    txt = open(HEADER).read()
-    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(shud_rhs_\w+)\s*\(", txt)))
+def header_functions(header=None):
+    names = set()
+    for h, (prefix, _) in HEADERS.items():
+        if header and h != header:
+            continue
+        txt = open(os.path.join(ROOT, "include", h)).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        names |= set(re.findall(r"\b(" + prefix + r"\w+)\s*\(", txt))
+    return sorted(names)
 
 
 def test_header_functions_all_bound():
-    names = header_functions()
-    assert len(names) >= 20
-    assert set(names) == set(abi.FUNCTIONS), set(names) ^ set(abi.FUNCTIONS)
+    for h, (_, table) in HEADERS.items():
+        names = header_functions(h)
+        assert len(names) >= 4
+        assert set(names) == set(table), (h, set(names) ^ set(table))
 
 
 def test_library_exports_every_symbol():
@@ -35,7 +41,7 @@ def test_library_exports_every_symbol():
 
 
 def _c_sizeof(struct):
-    src = f'#include "shud_rhs.h"\n#include <stdio.h>\nint main(){{printf("%zu\\n", sizeof({struct}));return 0;}}\n'
+    src = f'#include "shud_rhs.h"\n#include "shud_et.h"\n#include <stdio.h>\nint main(){{printf("%zu\\n", sizeof({struct}));return 0;}}\n'
     exe = f"/tmp/sz_{struct}_{os.getpid()}"
     subprocess.run(["gcc", "-x", "c", "-", "-I", os.path.join(ROOT, "include"), "-o", exe], input=src.encode(),
                    check=True)
@@ -48,5 +54,7 @@ def test_struct_layouts_match_header():
     for name, cls in [("ShudMeshSoA", abi.ShudMeshSoA), ("ShudParamsSoA", abi.ShudParamsSoA),
                       ("ShudStepInputs", abi.ShudStepInputs), ("ShudRhsOptions", abi.ShudRhsOptions),
                       ("ShudFluxOut", abi.ShudFluxOut), ("ShudErr", abi.ShudErr),
-                      ("ShudPartition", abi.ShudPartition)]:
+                      ("ShudPartition", abi.ShudPartition), ("ShudEtMeshSoA", abi.ShudEtMeshSoA),
+                      ("ShudEtParams", abi.ShudEtParams), ("ShudEtForcing", abi.ShudEtForcing),
+                      ("ShudEtOut", abi.ShudEtOut)]:
         assert C.sizeof(cls) == _c_sizeof(name), name
