@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-reps", type=int, default=20)
     ap.add_argument("--host-vectors", action="store_true", help="also time the PCIe-inclusive host-vector eval")
+    ap.add_argument("--no-et", action="store_true", help="skip the ET-step prelude timing (SURVEY f1)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -185,6 +186,9 @@ def main():
             h.eval(0.0, y_h, dy_h, raise_on_physics=False)
         out["host_vector_value"] = NE * nrep / (time.perf_counter() - th)
 
+    if world == 1 and not args.no_et:
+        out["et_prelude"] = et_prelude_timing(h, gm)
+
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(gm, y_glob, mode, args.cpu_seconds)
     if world > 1:
@@ -194,6 +198,27 @@ def main():
     h.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def et_prelude_timing(h, gm, reps=10):
+    """The ET-step prelude on the device (shud_et_step) on the same mesh: synthetic statics and
+    forcing rows (4 stations, terrain radiation recomputed each step), once per ET step — not per RHS.  Each
+    call ends with the error-word read, like the reference's myexit checks."""
+    from shud_rhs import abi, et
+    etm = et.synth_et(gm.num_ele, seed=4)
+    h.et_attach(etm)
+    fs = [et.synth_forcing(60.0 * k, 60.0, seed=k, tsr_mode=abi.SHUD_TSR_RECOMPUTE) for k in range(reps + 3)]
+    for f in fs[:3]:
+        h.et_step(f)
+    t0 = time.perf_counter()
+    for f in fs[3:]:
+        h.et_step(f)
+    ms = (time.perf_counter() - t0) / reps * 1e3
+    # bytes the kernel moves per element: statics 92 + carried r/w 48 + outputs 16x8 + packed records 40
+    b_ele = 92 + 48 + 128 + 40
+    return {"ms_per_step": ms, "bytes_per_element": b_ele, "achieved_GBs": b_ele * gm.num_ele / (ms * 1e-3) / 1e9,
+            "note": "per ET step (not per RHS); replaces a 56 B/element host->device upload of step inputs "
+                    "plus the host's tReadForcing/ET loops"}
 
 
 def stream_copy_gbs(dev, n=1 << 28, reps=20):
