@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--profile-reps", type=int, default=20)
     ap.add_argument("--host-vectors", action="store_true", help="also time the PCIe-inclusive host-vector eval")
     ap.add_argument("--no-et", action="store_true", help="skip the ET-step prelude timing (SURVEY f1)")
+    ap.add_argument("--partition-1", action="store_true",
+                    help="run the N>1 code path (partitioned handle, RCCL comm, overlap) with one rank (smoke test)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -70,12 +72,13 @@ def main():
     log(f"[bench] syn mesh NE={NE} NR={NR} NS={NS} built in {time.time() - t0:.1f}s")
 
     stream = torch.cuda.current_stream()
-    if world > 1:
+    if world > 1 or args.partition_1:
         ele_part, _, plans = partition.build_plans(gm, world)
         cut_e, cut_s = partition.edge_cut(gm, ele_part)
         lm, part = partition.local_model(gm, plans[rank], rank, world)
         uid = [runtime.nccl_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0)
         part.nccl_unique_id = uid[0]
         h = runtime.RhsHandle(lm, mode=mode, device=local, stream=stream.cuda_stream, partition=part)
         y_loc = partition.local_state(y_glob, gm, part)

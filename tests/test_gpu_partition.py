@@ -67,3 +67,33 @@ def test_partitioned_handles_bit_identical(nranks, mode, packed, monkeypatch):
             h.device_free(a)
             h.device_free(b)
             h.close()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_rccl_comm_single_rank(mode):
+    """The RCCL transport path (comm init from a unique id, comm stream + events, interior/boundary launch
+    split) on a one-rank partition: must equal the unpartitioned handle bit for bit.  (N > 1 RCCL needs one
+    GPU per rank; the multi-rank data movement itself is covered by the D2D-transport test above.)"""
+    from shud_rhs import runtime as rt
+    m, y = cases.variant(20000, seed=17)
+    single = rt.RhsHandle(m, mode=mode)
+    single.set_step_inputs()
+    _, _, plans = partition.build_plans(m, 1)
+    lm, part = partition.local_model(m, plans[0], 0, 1)
+    part.nccl_unique_id = rt.nccl_unique_id()
+    h = rt.RhsHandle(lm, mode=mode, partition=part)
+    h.set_step_inputs()
+    ny = 3 * part.n_own_ele + part.n_own_riv
+    dy_, ddy = h.device_alloc(8 * ny), h.device_alloc(8 * ny)
+    try:
+        for yy in [y, workload.random_state(m, seed=4)]:
+            for call in range(3):
+                ref = single.eval(0.0, yy)
+                h.h2d(dy_, partition.local_state(yy, m, part))
+                h.eval_device(0.0, dy_, ddy)
+                got = h.d2h(np.zeros(ny), ddy)
+                assert np.array_equal(got, partition.local_state(ref, m, part)), f"call {call}"
+    finally:
+        h.device_free(dy_)
+        h.device_free(ddy)
+        h.close()
