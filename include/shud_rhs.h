@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SHUD_RHS_ABI_VERSION 1
+#define SHUD_RHS_ABI_VERSION 2   /* 2: lakes (ShudMeshSoA/ShudStepInputs/ShudFluxOut tails) */
 
 /* ---- return codes (CVODE convention: 0 ok, <0 unrecoverable, >0 recoverable) ---- */
 #define SHUD_OK              0
@@ -73,7 +73,7 @@ typedef struct ShudMeshSoA {
     const double  *rough;          /* [NE]  Landcover::Rough, read only when close_boundary == 0  */
     const int32_t *ibc;            /* [NE]  AttriuteIndex::iBC                                    */
     const int32_t *iss;            /* [NE]  AttriuteIndex::iSS                                    */
-    const int32_t *ilake;          /* [NE]  AttriuteIndex::iLake (must be <= 0), may be NULL      */
+    const int32_t *ilake;          /* [NE]  AttriuteIndex::iLake (> 0: lake element), may be NULL */
     /* river reaches (_River, River.hpp:47-93) */
     const int32_t *riv_down;       /* [NR]                                                        */
     const int32_t *riv_bc;         /* [NR]  _River::BC                                            */
@@ -91,6 +91,14 @@ typedef struct ShudMeshSoA {
     const int32_t *seg_riv;        /* [NS]  0-based reach                                         */
     const double  *seg_length;     /* [NS]                                                        */
     const double  *seg_cwr;        /* [NS]                                                        */
+    /* lakes (MD_Lake.cpp, Lake.hpp/.cpp).  Lakes are on when any ilake > 0 (MD_readin.cpp:
+     * 262-263); lake ids are 1..num_lake; a reach with riv_down <= -4 then flows into lake (-3 - down)
+     * (MD_Lake.cpp:46-50) instead of the critical-depth outlet.  The y/ydot vectors gain num_lake stages
+     * after the reaches ([sf|us|gw|riv|lake], Macros.hpp:21-25).  Serial semantics, unpartitioned only. */
+    int32_t num_lake;
+    const int32_t *lake_bathy_off; /* [num_lake+1] row offsets of each lake's bathymetry table       */
+    const double  *lake_bathy_y;   /* LakeBathymetry::yi (stage datum; zmin = yi[0]), lake_readBathy */
+    const double  *lake_bathy_a;   /* LakeBathymetry::ai (top area)                                 */
 } ShudMeshSoA;
 
 /* Per-element hydraulic parameters after calibration and init (Soil_Layer / Geol_Layer /
@@ -122,6 +130,7 @@ typedef struct ShudStepInputs {
     const double *ele_qbc; int32_t n_ele_qbc;   /* tsd_eqBC, indexed by -iBC  (iBC < 0) */
     const double *riv_ybc; int32_t n_riv_ybc;   /* tsd_ryBC, indexed by  BC   (BC > 0)  */
     const double *riv_qbc; int32_t n_riv_qbc;   /* tsd_rqBC, indexed by -BC   (BC < 0)  */
+    const double *prcp;       /* qElePrep [NE]: precipitation of lake elements (MD_f.cpp:17)    */
 } ShudStepInputs;
 
 typedef struct ShudRhsOptions {
@@ -145,6 +154,8 @@ typedef struct ShudFluxOut {
     double *qe2r_surf, *qe2r_sub;                    /* [NE] */
     double *qseg_surf, *qseg_sub;                    /* [NS] reference segment order */
     double *qriv_down, *qriv_up, *qriv_surf, *qriv_sub; /* [NR] */
+    double *q_lake_surf, *q_lake_sub, *q_lake_rivin; /* QLakeSurf/QLakeSub/QLakeRivIn [num_lake]       */
+    double *q_lake_evap, *q_lake_prcp, *lake_toparea; /* qLakeEvap/qLakePrcp, y2LakeArea [num_lake]   */
 } ShudFluxOut;
 
 typedef struct ShudErr {

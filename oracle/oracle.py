@@ -71,6 +71,8 @@ class OracleRhs:
         self._mesh = model.mesh_struct()
         self._par = model.params_struct()
         self.h = lib().oracle_create(C.byref(self._mesh), C.byref(self._par), int(mode))
+        if not self.h:
+            raise ValueError("oracle: unsupported configuration (lakes need serial mode)")
         self.mode = mode
 
     def __del__(self):
@@ -100,7 +102,8 @@ class OracleRhs:
         NE, NR, NS = m.num_ele, m.num_riv, m.num_seg
         out, o = {}, abi.ShudFluxOut()
         for name in abi.FLUXOUT_ORDER:
-            n = 3 * NE if name in abi.DIAG_ELE3 else NS if name in abi.DIAG_SEG else NR if name in abi.DIAG_RIV else NE
+            n = (3 * NE if name in abi.DIAG_ELE3 else NS if name in abi.DIAG_SEG else NR if name in abi.DIAG_RIV
+                 else getattr(m, "num_lake", 0) if name in abi.DIAG_LAKE else NE)
             out[name] = np.zeros(n)
             setattr(o, name, out[name].ctypes.data_as(abi.c_double_p))
         lib().oracle_get_diag(self.h, C.byref(o))

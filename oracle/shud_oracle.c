@@ -46,6 +46,7 @@ static inline double rmax(double a, double b) { return (a < b ? b : a); }
 
 typedef struct OracleModel {
     int NE, NR, NS, mode, close_boundary;
+    int NL, lakeon;                              /* lakes (MD_Lake.cpp; Model_Data.hpp:182-191) */
     /* static mesh (owned copies) */
     int *nabr;                                   /* [NE*3] element-major, 0-based / -1 */
     double *area, *z_surf, *z_bottom, *depression, *edge, *dist2nabor, *dist2edge, *avg_rough, *rough;
@@ -55,6 +56,10 @@ typedef struct OracleModel {
            *riv_bankslope, *riv_ksath, *riv_bedthick;
     int *seg_ele, *seg_riv;
     double *seg_length, *seg_cwr;
+    /* lakes: ids, _Element::lakenabr (MD_Lake.cpp:131-143), _River::toLake (:44-52), bathymetry, state */
+    int *ilake, *lakenabr, *NumEleLake, *toLake, *lake_off;
+    double *lake_y, *lake_a, *qElePrep, *yLakeStg, *y2LakeArea, *QLakeSurf, *QLakeSub, *QLakeRivIn, *QLakeRivOut,
+           *qLakeEvap, *qLakePrcp, *lakeQsub;
     /* element params */
     double *AquiferDepth, *macD, *macKsatH, *geo_vAreaF, *KsatH, *KsatV, *infKsatV, *hAreaF,
            *macKsatV, *ThetaS, *ThetaR, *Beta, *infD, *Sy, *RzD, *VegFrac, *ImpAF;
@@ -107,6 +112,7 @@ int oracle_get_threads(void) {
 #define NT (g_threads > 0 ? g_threads : omp_get_max_threads())
 #endif
 
+void oracle_destroy(OracleModel *M);
 OracleModel *oracle_create(const ShudMeshSoA *m, const ShudParamsSoA *p, int mode) {
     OracleModel *M = (OracleModel *)calloc(1, sizeof(OracleModel));
     int NE = m->num_ele, NR = m->num_riv, NS = m->num_seg;
@@ -156,7 +162,36 @@ OracleModel *oracle_create(const ShudMeshSoA *m, const ShudParamsSoA *p, int mod
     M->r_TopArea = zeros(NR); M->r_qBC = zeros(NR); M->r_yBC = zeros(NR);
     M->QrivSurf = zeros(NR); M->QrivSub = zeros(NR); M->QrivDown = zeros(NR); M->QrivUp = zeros(NR);
     M->QsegSurf = zeros(NS); M->QsegSub = zeros(NS);
+    /* lakes: lakeon when any iLake > 0 (MD_readin.cpp:262-263), NumLake = LakeUniqueID (MD_Lake.cpp:12-29) */
+    int NL = m->num_lake > 0 ? m->num_lake : 0;
+    M->NL = NL;
+    M->ilake = dup_i(m->ilake, NE, 0);
+    for (int i = 0; i < NE; i++) if (M->ilake[i] > 0) M->lakeon = 1;
+    M->lakenabr = (int *)calloc(3 * (NE ? NE : 1), sizeof(int));
+    M->NumEleLake = (int *)calloc(NL ? NL : 1, sizeof(int));
+    M->toLake = (int *)malloc(sizeof(int) * (NR ? NR : 1));
+    M->lake_off = dup_i(m->lake_bathy_off, NL + 1, 0);
+    int nb = NL ? M->lake_off[NL] : 0;
+    M->lake_y = dup_d(m->lake_bathy_y, nb, 0); M->lake_a = dup_d(m->lake_bathy_a, nb, 0);
+    M->qElePrep = zeros(NE); M->lakeQsub = zeros(3 * NE);
+    M->yLakeStg = zeros(NL); M->y2LakeArea = zeros(NL); M->QLakeSurf = zeros(NL); M->QLakeSub = zeros(NL);
+    M->QLakeRivIn = zeros(NL); M->QLakeRivOut = zeros(NL); M->qLakeEvap = zeros(NL); M->qLakePrcp = zeros(NL);
+    for (int i = 0; i < NR; i++)                                   /* MD_Lake.cpp:44-52 */
+        M->toLake[i] = (M->lakeon && M->riv_down[i] <= -4) ? (-3 - M->riv_down[i]) - 1 : NA_VALUE;
+    if (M->lakeon) {
+        for (int i = 0; i < NE; i++) if (M->ilake[i] > 0 && M->ilake[i] <= NL) M->NumEleLake[M->ilake[i] - 1]++;
+        for (int i = 0; i < NE; i++)                               /* MD_Lake.cpp:131-143 */
+            if (M->ilake[i] <= 0)
+                for (int j = 0; j < 3; j++) {
+                    int inabr = M->nabr[i * 3 + j];
+                    if (inabr >= 0 && M->ilake[inabr] > 0) M->lakenabr[i * 3 + j] = M->ilake[inabr];
+                }
+    }
     M->quiet = 1;
+    if (M->lakeon && mode == SHUD_MODE_OMP) {   /* the OMP path has no lake physics: not restated */
+        oracle_destroy(M);
+        return NULL;
+    }
     return M;
 }
 
@@ -176,6 +211,7 @@ void oracle_set_step_inputs(OracleModel *M, const ShudStepInputs *in) {
     set_arr(M->qPotTran, in->pot_tran, NE); set_arr(M->qEleETP, in->etp, NE);
     set_arr(M->t_lai, in->lai, NE); set_arr(M->fu_Surf, in->fu_surf, NE); set_arr(M->fu_Sub, in->fu_sub, NE);
     set_arr(M->qEleE_IC, in->e_ic, NE); set_arr(M->u_satn, in->u_satn, NE);
+    set_arr(M->qElePrep, in->prcp, NE);
     /* uYgw of iBC<0 elements is never refreshed by f_update (MD_update.cpp:123-125) */
     if (in->ugw_stale)
         for (int i = 0; i < NE; i++) if (M->ibc[i] < 0) M->uYgw[i] = in->ugw_stale[i];
@@ -433,6 +469,48 @@ static int f_etFlux(OracleModel *M, int i, int *warn) {
 }
 
 /* MD_update.cpp:102-189 Model_Data::f_update (serial) */
+/* Lake.cpp:59-79 LakeBathymetry::toparea (the reference's own interpolation, kept as written) */
+static double lake_toparea(OracleModel *M, int l, double y) {
+    const double *yi = M->lake_y + M->lake_off[l], *ai = M->lake_a + M->lake_off[l];
+    int nvalue = M->lake_off[l + 1] - M->lake_off[l];
+    double ta = ai[0], dy, da;
+    if (y <= yi[0]) {
+        ta = ai[0];
+    } else {
+        for (int i = 1; i < nvalue; i++) {
+            if (y < yi[i]) {
+                da = (ai[i] - ta);
+                dy = yi[i] - y;
+                ta = da / dy * (y - yi[i - 1]) + ta;
+                break;
+            } else {
+                ta = ai[i];
+            }
+        }
+    }
+    return ta;
+}
+/* Element.cpp:336-346 _Element::updateLakeElement */
+static void updateLakeElement(OracleModel *M, int i) {
+    M->u_effKH[i] = M->KsatH[i];
+    M->u_deficit[i] = 0;
+    M->Kmax[i] = M->infKsatV[i];
+    M->u_deficit[i] = 0.;
+    M->u_satn[i] = 1.;
+    M->u_theta[i] = M->ThetaS[i];
+    M->u_satKr[i] = 1.0;
+    M->u_phius[i] = 0.;
+    M->u_effkInfi[i] = M->infKsatV[i];
+}
+/* MD_ElementFlux.cpp:2-17 Model_Data::fun_Ele_lakeVertical */
+static void fun_Ele_lakeVertical(OracleModel *M, int i) {
+    M->qEleInfil[i] = 0.; M->qEleRecharge[i] = 0.; M->qEleExfil[i] = 0.; M->qEleTrans[i] = 0.;
+    M->qEs[i] = 0.; M->qEu[i] = 0.; M->qEg[i] = 0.; M->qTu[i] = 0.; M->qTg[i] = 0.;
+    M->qEleE_IC[i] = 0.; M->qEleTrans[i] = 0.;
+    M->qEleEvapo[i] = M->qPotEvap[i];
+    M->qEleETA[i] = M->qEleE_IC[i] + M->qEleEvapo[i] + M->qEleTrans[i];
+}
+
 static void f_update(OracleModel *M, const double *Y, double *DY, double t) {
     (void)t;
     int NE = M->NE, NR = M->NR;
@@ -468,7 +546,13 @@ static void f_update(OracleModel *M, const double *Y, double *DY, double t) {
     }
     for (int i = 0; i < NR; i++) { M->QrivSurf[i] = 0.; M->QrivSub[i] = 0.; M->QrivUp[i] = 0.; }
     for (int i = 0; i < NE; i++) { M->Qe2r_Surf[i] = 0.; M->Qe2r_Sub[i] = 0.; }
-    for (int i = 0; i < 3 * NE + NR; i++) DY[i] = 0.;
+    for (int i = 0; i < M->NL; i++) {                         /* MD_update.cpp:174-185 */
+        M->yLakeStg[i] = Y[3 * NE + NR + i];
+        M->y2LakeArea[i] = lake_toparea(M, i, M->yLakeStg[i] + M->lake_y[M->lake_off[i]]);   /* _Lake::update */
+        M->QLakeSub[i] = 0.; M->QLakeSurf[i] = 0.; M->qLakeEvap[i] = 0.; M->qLakePrcp[i] = 0.;
+        M->QLakeRivIn[i] = 0.; M->QLakeRivOut[i] = 0.;
+    }
+    for (int i = 0; i < 3 * NE + NR + M->NL; i++) DY[i] = 0.;
 }
 
 /* MD_f_omp.cpp:104-170 Model_Data::f_update_omp */
@@ -519,15 +603,22 @@ static void fun_Ele_Recharge(OracleModel *M, int i) {
     M->qEleRecharge[i] = Flux_Recharge(M, i, M->uYus[i], M->uYgw[i]);
     M->qEleRecharge[i] *= M->fu_Sub[i];
 }
-/* MD_ElementFlux.cpp:35-97 (lake branch out of scope) */
+static double WeirFlow_jtoi(double zi, double yi, double zj, double yj, double zbank, double cwr,
+                            double width, double threshold);
+/* MD_ElementFlux.cpp:35-97 (QLakeSurf is accumulated by f_loop in reference order) */
 static void fun_Ele_surface(OracleModel *M, int i) {
     double Ymean, dh, s, CrossA, Q, B, isf, nsf;
     isf = M->uYsf[i];
     isf = isf < 0. ? 0. : isf;
     for (int j = 0; j < 3; j++) {
         int inabr = M->nabr[i * 3 + j];
+        int ilake = M->lakenabr[i * 3 + j] - 1;
         B = M->edge[i * 3 + j];
-        if (inabr >= 0) {
+        if (ilake >= 0) {                            /* bank edge: weir to the lake (:46-53) */
+            nsf = M->yLakeStg[ilake];
+            nsf = nsf < 0. ? 0. : nsf;
+            Q = WeirFlow_jtoi(M->lake_y[M->lake_off[ilake]], nsf, M->z_surf[i], isf, M->z_surf[i], 0.6, B, 0.01);
+        } else if (inabr >= 0) {
             nsf = M->uYsf[inabr];
             nsf = nsf < 0. ? 0. : nsf;
             dh = (isf + M->z_surf[i]) - (nsf + M->z_surf[inabr]);
@@ -554,12 +645,25 @@ static void fun_Ele_surface(OracleModel *M, int i) {
         M->QeleSurf[i * 3 + j] = Q;
     }
 }
-/* MD_ElementFlux.cpp:100-156 (lake branch out of scope) */
+/* MD_ElementFlux.cpp:100-156 (QLakeSub is accumulated by f_loop in reference order) */
 static void fun_Ele_sub(OracleModel *M, int i) {
     double Ymean, dh, Kmean, grad, Q;
     for (int j = 0; j < 3; j++) {
         int inabr = M->nabr[i * 3 + j];
-        if (inabr >= 0) {
+        int ilake = M->lakenabr[i * 3 + j] - 1;
+        if (ilake >= 0) {                            /* bank edge: Darcy to the lake (:107-121) */
+            double zl = M->lake_y[M->lake_off[ilake]], yl = M->yLakeStg[ilake];
+            dh = (M->uYgw[i] + M->z_bottom[i]) - (yl + zl);
+            if (dh > 0. && M->uYgw[i] <= 0.02) Q = 0.;
+            else if (dh < 0. && yl <= 0.02) Q = 0.;
+            else {
+                Ymean = avgY_gw(M->z_bottom[i], M->uYgw[i], zl, yl, 0.002);
+                grad = dh / M->dist2nabor[i * 3 + j];
+                Kmean = 0.5 * (M->u_effKH[i] + M->u_effKH[inabr]);   /* the lake element's KsatH */
+                Q = Kmean * grad * Ymean * M->edge[i * 3 + j];
+            }
+            M->lakeQsub[i * 3 + j] = Q;
+        } else if (inabr >= 0) {
             dh = (M->uYgw[i] + M->z_bottom[i]) - (M->uYgw[inabr] + M->z_bottom[inabr]);
             if (dh > 0. && M->uYgw[i] <= 0.02) Q = 0.;
             else if (dh < 0. && M->uYgw[inabr] <= 0.02) Q = 0.;
@@ -618,12 +722,18 @@ static void fun_Seg_sub(OracleModel *M, int iEle, int iRiv, int i) {
                                 M->riv_bedthick[iRiv]);
     M->QsegSub[i] *= M->fu_Sub[iEle];
 }
-/* MD_RiverFlux.cpp:5-63 (lake branch out of scope; invalid `down` rejected at create) */
+/* MD_RiverFlux.cpp:5-63 (QLakeRivIn is accumulated by f_loop in reach order; invalid `down` rejected) */
 static void Flux_RiverDown(OracleModel *M, int i) {
     double Distance, CSarea, Perem, R, s, n, sMean = 0.;
     int iDown = M->riv_down[i];
     n = M->riv_avg_rough[i];
-    if (iDown >= 0) {
+    if (M->toLake[i] >= 0) {                          /* to a lake (:17-25) */
+        Perem = M->r_CSperem[i];
+        s = M->riv_bed_slope[i] + M->uYriv[i] * 2. / M->riv_length[i];
+        CSarea = M->r_CSarea[i];
+        R = (Perem <= 0.) ? 0. : (CSarea / Perem);
+        M->QrivDown[i] = ManningEquation(CSarea, n, R, s);
+    } else if (iDown >= 0) {
         sMean = (M->riv_bed_slope[i] + M->riv_bed_slope[iDown]) * 0.5;
         Distance = M->riv_dist2down[i];
         s = ((M->uYriv[i] - M->riv_depth[i]) - (M->uYriv[iDown] - M->riv_depth[iDown])) / Distance + sMean;
@@ -672,6 +782,11 @@ static int f_loop(OracleModel *M) {
 #pragma omp parallel for num_threads(NT) schedule(static) reduction(+ : nwarn)
     for (int i = 0; i < NE; i++) {
         int bad = 0, warn = 0;
+        if (M->lakeon && M->ilake[i] > 0) {          /* lake element (MD_f.cpp:12-17) */
+            updateLakeElement(M, i);
+            fun_Ele_lakeVertical(M, i);
+            continue;
+        }
         if (!omp) {
             int k = f_etFlux(M, i, &warn);
             nwarn += warn;
@@ -691,12 +806,31 @@ static int f_loop(OracleModel *M) {
             return M->exit_code;
         }
     free(aerr);
+    for (int i = 0; i < NE; i++)                            /* MD_f.cpp:16-17, element order */
+        if (M->lakeon && M->ilake[i] > 0) {
+            int l = M->ilake[i] - 1;
+            M->qLakeEvap[l] += M->qEleEvapo[i] / M->NumEleLake[l];
+            M->qLakePrcp[l] += M->qElePrep[i] / M->NumEleLake[l];
+        }
     /* loop B (MD_f.cpp:27-36) */
 #pragma omp parallel for num_threads(NT) schedule(static)
     for (int i = 0; i < NE; i++) {
+        if (M->lakeon && M->ilake[i] > 0) {          /* fun_Ele_lakeHorizon (MD_ElementFlux.cpp:18-23) */
+            for (int j = 0; j < 3; j++) { M->QeleSurf[i * 3 + j] = 0.; M->QeleSub[i * 3 + j] = 0.; }
+            continue;
+        }
         fun_Ele_surface(M, i);
         fun_Ele_sub(M, i);
     }
+    if (M->lakeon)                                            /* QLakeSurf/QLakeSub, element then edge order */
+        for (int i = 0; i < NE; i++)
+            for (int j = 0; j < 3; j++) {
+                int l = M->lakenabr[i * 3 + j] - 1;
+                if (l >= 0 && M->ilake[i] <= 0) {
+                    M->QLakeSurf[l] += M->QeleSurf[i * 3 + j];
+                    M->QLakeSub[l] += M->lakeQsub[i * 3 + j];
+                }
+            }
     /* loop C (MD_f.cpp:37-40) */
 #pragma omp parallel for num_threads(NT) schedule(static)
     for (int i = 0; i < NS; i++) {
@@ -706,6 +840,12 @@ static int f_loop(OracleModel *M) {
     /* loop D (MD_f.cpp:41-43) */
 #pragma omp parallel for num_threads(NT) schedule(static)
     for (int i = 0; i < NR; i++) Flux_RiverDown(M, i);
+    for (int i = 0; i < NR; i++)                              /* MD_RiverFlux.cpp:24, reach order */
+        if (M->toLake[i] >= 0) M->QLakeRivIn[M->toLake[i]] += M->QrivDown[i];
+    for (int i = 0; i < M->NL; i++) {                         /* MD_f.cpp:44-47 */
+        M->qLakeEvap[i] = rmin(M->qLakeEvap[i], M->qLakePrcp[i] + M->yLakeStg[i]);
+        M->qLakeEvap[i] = rmax(0, M->qLakeEvap[i]);
+    }
     PassValue(M);                                             /* MD_f.cpp:49 */
     return 0;
 }
@@ -743,6 +883,7 @@ static int f_applyDY(OracleModel *M, double *DY) {
         else DY[igw] += 0.0 / area;
         DY[ius] /= M->Sy[i];
         DY[igw] /= M->Sy[i];
+        if (M->ilake[i] > 0) { DY[isf] = 0.; DY[ius] = 0.; DY[igw] = 0.; }   /* MD_f.cpp:146-150 */
     }
 #pragma omp parallel for num_threads(NT) schedule(static)
     for (int i = 0; i < NR; i++) {
@@ -755,6 +896,9 @@ static int f_applyDY(OracleModel *M, double *DY) {
             DY[iriv] = fun_dAtodY(DY[iriv], M->r_topWidth[i], M->riv_bankslope[i]);
         }
     }
+    for (int i = 0; i < M->NL; i++)                           /* MD_f.cpp:180-190 */
+        DY[3 * NE + NR + i] = M->qLakePrcp[i] - M->qLakeEvap[i] +
+                              (M->QLakeRivIn[i] - M->QLakeRivOut[i] + M->QLakeSub[i] + M->QLakeSurf[i]) / M->y2LakeArea[i];
     return 0;
 }
 /* MD_f_omp.cpp:9-67 Model_Data::f_applyDY_omp (race-free restatement of the shared area/isf/ius/igw) */
@@ -828,6 +972,10 @@ void oracle_get_diag(OracleModel *M, ShudFluxOut *o) {
     cp_out(o->qseg_surf, M->QsegSurf, NS); cp_out(o->qseg_sub, M->QsegSub, NS);
     cp_out(o->qriv_down, M->QrivDown, NR); cp_out(o->qriv_up, M->QrivUp, NR);
     cp_out(o->qriv_surf, M->QrivSurf, NR); cp_out(o->qriv_sub, M->QrivSub, NR);
+    int NL = M->NL;
+    cp_out(o->q_lake_surf, M->QLakeSurf, NL); cp_out(o->q_lake_sub, M->QLakeSub, NL);
+    cp_out(o->q_lake_rivin, M->QLakeRivIn, NL); cp_out(o->q_lake_evap, M->qLakeEvap, NL);
+    cp_out(o->q_lake_prcp, M->qLakePrcp, NL); cp_out(o->lake_toparea, M->y2LakeArea, NL);
 }
 
 void oracle_destroy(OracleModel *M) {

@@ -21,7 +21,7 @@ struct DevMesh {
     const double *aq, *macD, *macKsatH, *vAreaF, *KsatH, *KsatV, *infKsatV, *hAreaF, *macKsatV;
     const double *ThetaS, *ThetaR, *Beta, *infD, *Sy, *RzD, *VegFrac, *ImpAF;
     // per-ET-step inputs
-    const double *net_prep, *pot_evap, *pot_tran, *etp, *lai, *fu_surf, *fu_sub;
+    const double *net_prep, *pot_evap, *pot_tran, *etp, *lai, *fu_surf, *fu_sub, *prcp;
     double *e_ic[2], *u_satn[2];     // carried state, ping-pong (read [cur], write [cur^1])
     const double *ugw_stale;
     const double *eybc, *eqbc, *rybc, *rqbc;
@@ -67,7 +67,8 @@ struct DevPacked {
     int ncls;
     const double2 *zz;      // {z_surf, z_bottom}  (aquifer_depth == z_surf - z_bottom, checked at create)
     const int4 *meta;       // {nabr0, nabr1, nabr2, cf}: cf bits 0-7 iBC (int8), 8-9 iSS class,
-                            //   10-15 #river segments, 16-31 class id  (zz and meta.w are neighbour-gathered)
+                            //   10-15 #river segments, 16-30 class id, 31 lake element
+                            //   (zz and meta.w are neighbour-gathered)
     const double2 *ged;     // [3][NE] edge-major {edge_j, dist2nabor_j}
     const double *area;
     const int *seg_first;   // first element-sorted segment of each element
@@ -93,6 +94,23 @@ struct DevDiag {                     // optional diagnostic outputs (ShudFluxOut
     double *qele_surf, *qele_sub, *qele_surf_tot, *qele_sub_tot, *q_infil, *q_exfil, *q_recharge;
     double *q_es, *q_eu, *q_eg, *q_tu, *q_tg, *q_eta, *e_ic, *u_satn, *i_beta, *eff_kh;
     double *qe2r_surf, *qe2r_sub, *qriv_down, *qriv_up, *qriv_surf, *qriv_sub;
+    double *q_lake_surf, *q_lake_sub, *q_lake_rivin, *q_lake_evap, *q_lake_prcp, *lake_toparea;
+};
+
+// ---- lakes (serial semantics, unpartitioned, packed layout) ----------------------------
+// Lake elements carry bit 31 of DevPacked::meta.w; a non-lake element's edge whose neighbour has it is a
+// bank edge (lakenabr, MD_Lake.cpp:131-143).  The element kernel writes each bank edge's fluxes; the lake
+// kernel reduces them, the lake elements' PET/precipitation and the inflowing reaches in reference order.
+struct DevLake {
+    int nl;
+    int y_off;                       // first lake stage in y / ydot (3 NE + NR)
+    const int *lake_of;              // [NE] 0-based lake of a lake element
+    double *bank_qs, *bank_qg;       // [3][NE] bank-edge surface weir Q and subsurface Q (before fu_Sub)
+    const int *bathy_off;            // [nl+1] LakeBathymetry rows
+    const double *bathy_y, *bathy_a;
+    const int *ele_off, *ele_idx;    // lake elements of each lake, ascending
+    const int *bank_off, *bank_pos;  // bank edges of each lake, element then edge order; pos = j*NE + i
+    const int *rin_off, *rin_idx;    // reaches flowing into each lake (toLake), ascending
 };
 
 // state accessors: owned entities read the caller's y, ghosts read the halo buffers
@@ -113,9 +131,11 @@ void launch_element_kernel(const DevMesh &m, const YView &Y, double *dy, int n_c
                            int mode, bool open, bool diag, const DevDiag &dg, hipStream_t s, int variant = 0);
 void launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1,
                                   int cur, int mode, bool open, bool diag, bool fu_unit, const DevDiag &dg,
-                                  hipStream_t s);
+                                  hipStream_t s, const DevLake *lake = nullptr);
 void launch_river_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int mode,
                                 bool diag, const DevDiag &dg, hipStream_t s);
+void launch_lake_kernel(const DevMesh &m, const DevPacked &p, const DevLake &L, const YView &Y, double *dy,
+                        bool diag, const DevDiag &dg, hipStream_t s);
 void launch_pack_step_kernel(const DevMesh &m, const DevPacked &p, int n, int cur, unsigned what, hipStream_t s);
 void launch_river_kernel(const DevMesh &m, const YView &Y, double *dy, int mode, bool diag,
                          const DevDiag &dg, hipStream_t s);

@@ -46,7 +46,7 @@ __device__ __forceinline__ void stnt2(double2 *p, double a, double b) {
 __device__ __forceinline__ int cf_ibc(int cf) { return (int)(int8_t)(cf & 0xff); }
 __device__ __forceinline__ int cf_iss(int cf) { return (cf >> 8) & 3; }
 __device__ __forceinline__ int cf_nseg(int cf) { return (cf >> 10) & 63; }
-__device__ __forceinline__ int cf_class(int cf) { return (int)((unsigned)cf >> 16); }
+__device__ __forceinline__ int cf_class(int cf) { return (int)(((unsigned)cf >> 16) & 0x7fffu); }   // bit 31: lake
 
 // uYgw of element j (MD_update.cpp:114-125 / MD_f_omp.cpp:119-128)
 template <int MODE>
@@ -56,16 +56,8 @@ __device__ __forceinline__ double ugw_pk(const DevMesh &m, double ygw_raw, int i
     return m.ugw_stale[j];
 }
 
-#ifndef SHUD_ET_EARLY
-#define SHUD_ET_EARLY 1
-#endif
-#ifndef SHUD_EDGE_PIPE
-#define SHUD_EDGE_PIPE 0
-#endif
-struct EdgeIn { double2 g, nzz; int ncf; double nsf, ngw; };
-
-// class table staged in LDS (record-major [class][field], 144 B per class) when it has <= LDS_CLS_MAX classes:
-// the 18 + 3x5 class lookups per element become LDS reads with immediate offsets instead of dependent L2 trips
+// class table staged in LDS (record-major [class][field]) when it has <= LDS_CLS_MAX classes: the 18 + 3x5
+// class lookups per element become LDS reads with immediate offsets instead of dependent L2 trips
 #ifndef SHUD_LDS_CLS_MAX
 #define SHUD_LDS_CLS_MAX 128
 #endif
@@ -74,10 +66,14 @@ constexpr int LDS_CLS_MAX = SHUD_LDS_CLS_MAX;
 // different LDS banks (an even stride of 32 words put every class on one bank: ~960 conflict cycles/wave)
 constexpr int CF_LDS_STRIDE = CF_COUNT | 1;
 
-template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT>
+// LAKE: the model has lakes.  Lake elements (cf bit 31) follow updateLakeElement /
+// fun_Ele_lakeVertical / fun_Ele_lakeHorizon (Element.cpp:336-346, MD_ElementFlux.cpp:2-23) and get zero DY
+// (MD_f.cpp:146-150); bank edges of other elements exchange with the lake (MD_ElementFlux.cpp:46-53,107-121)
+// and leave their fluxes in DevLake for the lake kernel.  LAKE = false compiles all of it away.
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE>
 __global__ void __launch_bounds__(256, 5)
 shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int i0, int n_compute, int cur,
-                       DevDiag dg) {
+                       DevDiag dg, DevLake lk) {
     extern __shared__ double lct[];                       // ncls * CF_LDS_STRIDE doubles when LCT
     const int ncls = p.ncls;
     if (LCT) {
@@ -92,20 +88,19 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     const int NEl = m.num_ele;
     const int nown = Y.n_own;
 
-    // ---------------- state and static records first: saturation (and its two pow calls, the
-    // register peak) is computed while little else is live; ET's inputs are loaded after it ----------------
+    // ---------------- own records first; saturation (its two pow calls are the register peak) is computed
+    // while little else is live ----------------
     const int4 mt = p.meta[i];
     const double2 zz = p.zz[i];
     const double ysf_raw = Y.sf(i), yus_raw = Y.us(i), ygw_raw = Y.gw(i);
     const int cf = mt.w;
     const int cid = cf_class(cf), ibc = cf_ibc(cf);
-#if SHUD_ET_EARLY
+    const bool is_lake = LAKE && cf < 0;
     const double2 snp = ldnt2(&p.s_np[i]), stl = ldnt2(&p.s_tl[i]);
     const double etp = ldnt(&m.etp[i]);
     double2 fu;
     if (FU1) { fu.x = 1.0; fu.y = 1.0; } else fu = ldnt2(&p.s_fu[i]);
     const double2 csv = ldnt2(&p.cs[cur][i]);
-#endif
 #define CL(f) (LCT ? lct[cid * CF_LDS_STRIDE + CF_##f] : p.ctab[CF_##f * ncls + cid])
 #define CDIV(a, F) CDIV_(a, CL(F), CL(r_##F))
 
@@ -117,11 +112,13 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     const double aq = zs - zb;                    // InitElement after rmSinks (Model_Data.cpp:262-264)
 
     // ---- updateElement (Element.cpp:347-384); pure function of the state, hoisted above f_etFlux ----
-    const double ekh = eff_kh(ugw, aq, CL(macD), CL(macKsatH), CL(vAreaF), CL(KsatH));
-    report_w(m.err, ekh < 0. || ekh > 1e9, 0x02u, 1, i);
-    double deficit = aq - ugw;
-    double theta, satn, satkr;
-    {
+    double ekh, deficit, theta, satn, satkr;
+    if (is_lake) {                                // updateLakeElement (Element.cpp:336-346)
+        ekh = CL(KsatH); deficit = 0.; satn = 1.; theta = CL(ThetaS); satkr = 1.0;
+    } else {
+        ekh = eff_kh(ugw, aq, CL(macD), CL(macKsatH), CL(vAreaF), CL(KsatH));
+        report_w(m.err, ekh < 0. || ekh > 1e9, 0x02u, 1, i);
+        deficit = aq - ugw;
         const double ThS = CL(ThetaS), ThR = CL(ThetaR);
         if (deficit <= 0.) { deficit = 0.; satn = 1.; theta = ThS; }
         else { theta = SDIV(uus, deficit) * ThS; satn = CDIV(theta - ThR, dTh); }
@@ -132,13 +129,6 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         }
     }
 
-#if !SHUD_ET_EARLY
-    const double2 snp = ldnt2(&p.s_np[i]), stl = ldnt2(&p.s_tl[i]);
-    const double etp = ldnt(&m.etp[i]);
-    double2 fu;
-    if (FU1) { fu.x = 1.0; fu.y = 1.0; } else fu = ldnt2(&p.s_fu[i]);
-    const double2 csv = ldnt2(&p.cs[cur][i]);
-#endif
     const int sfirst = p.seg_first[i];
     const int iss = cf_iss(cf), nseg = cf_nseg(cf);
     const double infD = CL(infD), ThR = CL(ThetaR);
@@ -147,13 +137,15 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
 
     // ---- f_etFlux (MD_ET.cpp:343-404), serial semantics only (reads the previous call's u_satn) ----
     double Es = 0., Eu = 0., Eg = 0., Tu = 0., Tg = 0., eic = csv.y, ibeta = 0.;
-    if (MODE == 0) {
+    if (is_lake) {
+        eic = 0.;                                 // fun_Ele_lakeVertical: qEleE_IC = 0 (carried)
+        if (DIAG) { dg.q_es[i] = 0.; dg.q_eu[i] = 0.; dg.q_eg[i] = 0.; dg.q_tu[i] = 0.; dg.q_tg[i] = 0.;
+                    dg.q_eta[i] = 0. + snp.y + 0.; }
+    } else if (MODE == 0) {
         const double satn_prev = csv.x;
         const double va = CL(VegFrac), vb = CL(vb), pj = CL(pj);
         const double pet = snp.y, ptr = stl.x;
-        {
-            ibeta = soil_moisture_stress(CDIV(satn_prev * CL(dTh) - ThR, fcmr));   // fc = ThS * 0.75
-        }
+        ibeta = soil_moisture_stress(CDIV(satn_prev * CL(dTh) - ThR, fcmr));   // fc = ThS * 0.75
         Es = rmin(rmax(0., usf), pet) * vb;
         if (Es < pet) {
             if (ugw > aq - infD) { Eg = rmin(rmax(0., ugw), pet - Es) * pj * vb; Eu = 0.; }
@@ -179,11 +171,11 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
                     dg.q_eta[i] = eta; dg.i_beta[i] = ibeta; }
     }
     stnt2(&p.cs[cur ^ 1][i], satn, eic);
-    const double kmax = CL(kmax);
 
-    // ---- Flux_Infiltration (Element.cpp:271-303) ----
-    double qi = 0., qex = 0.;
-    {
+    // ---- Flux_Infiltration (Element.cpp:271-303) and Flux_Recharge (:304-335); zero on lake elements ----
+    double qi = 0., qex = 0., qr = 0.;
+    if (!is_lake) {
+        const double kmax = CL(kmax);
         const double av = usf + snp.x;
         if (ugw + uus > aq || deficit < uus) {
             qex = SDIV(fabs(ugw + uus - aq), aq) * kmax;
@@ -195,12 +187,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
             else ek = satkr * infK * CL(omh);
             qi = rmin(av, rmax(0., grad * ek));
         }
-    }
-    const double q_infil = qi * fu_surf, q_exfil = qex * fu_surf;
-    // ---- Flux_Recharge (Element.cpp:304-335), meanHarmonic (Equations.hpp:45-48) ----
-    double qr = 0.;
-    {
-        const double KV = CL(KsatV);
+        const double KV = CL(KsatV);                               // meanHarmonic, Equations.hpp:45-48
         if (!(ugw > aq - infD && uus < deficit)) {
             double grad = 0.;
             if (theta > ThR && !(uus <= K_EPSILON)) {
@@ -213,31 +200,16 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
             }
         }
     }
-    const double q_rech = qr * fu_sub;
+    const double q_infil = qi * fu_surf, q_exfil = qex * fu_surf;
+    const double q_rech = is_lake ? 0. : qr * fu_sub;
 
     // DY terms that do not depend on the lateral fluxes, in the reference's left-to-right order
     // (MD_f.cpp:88-90): dsf = ((net_prep - infil) + exfil) - Qsurf/area - Es,  dus complete,
     // dgw = (recharge - exfil) - Qsub/area - Eg - Tg.  Ends the ET/vertical live ranges early.
     const double dsf_head = snp.x - q_infil + q_exfil;
     const double dgw_head = q_rech - q_exfil;
-    if (i < nown) __builtin_nontemporal_store(CDIV(q_infil - q_rech - Eu - Tu, Sy), &dy[nown + i]);
+    if (i < nown) __builtin_nontemporal_store(is_lake ? 0. : CDIV(q_infil - q_rech - Eu - Tu, Sy), &dy[nown + i]);
 
-#if SHUD_EDGE_PIPE
-    auto load_edge = [&](int j) {
-        EdgeIn e;
-        const int nb = j == 0 ? mt.x : j == 1 ? mt.y : mt.z;
-        const int nc = nb >= 0 ? nb : i;                  // boundary edge: harmless in-bounds loads
-        e.g = ldnt2(&p.ged[(size_t)j * NEl + i]);
-        e.nzz = p.zz[nc];
-        e.ncf = p.meta[nc].w;
-        e.nsf = Y.sf(nc);
-        e.ngw = Y.gw(nc);
-        return e;
-    };
-#if SHUD_EDGE_PIPE == 2
-    const EdgeIn e0 = load_edge(0);                       // in flight across the segment loop
-#endif
-#endif
     // ---- own river segments (fun_Seg_surface / fun_Seg_sub) and Qe2r (PassValue) ----
     const double dep = CL(depression), rgh = CL(rough);
     double qe2r_surf = 0., qe2r_sub = 0.;
@@ -268,39 +240,42 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
 
     // ---- fun_Ele_surface / fun_Ele_sub, one edge per (rolled) iteration (MD_ElementFlux.cpp:35-156) ----
     // each edge's neighbour data is loaded at the top of its iteration; keeping the loop rolled holds the
-    // kernel at 96 VGPRs = 5 waves/SIMD (all three edges in flight at once needs ~145 = 3 waves: slower)
-#if SHUD_EDGE_PIPE == 1
-    const EdgeIn e0 = load_edge(0);
-#endif
+    // kernel at <= 96 VGPRs = 5 waves/SIMD (all three edges in flight at once needs ~145 = 3 waves: slower)
     double sumsurf = qe2r_surf, sumsub = qe2r_sub;     // QeleSurfTot = Qe2r + sum_j QeleSurf[j]
     bool nan_q = false;
     const double isf = usf < 0. ? 0. : usf;
-#if SHUD_EDGE_PIPE
-    // software-pipelined: edge j+1's neighbour records are in flight while edge j is computed
-    EdgeIn ein = e0;
 #pragma unroll 1
-    for (int j = 0; j < 3; j++) {
-        const int nb = j == 0 ? mt.x : j == 1 ? mt.y : mt.z;
-        const EdgeIn e = ein;
-        ein = load_edge(j < 2 ? j + 1 : 2);
-        const double2 g = e.g, nzz = e.nzz;
-        const int ncf = e.ncf;
-        const double nsf_raw = e.nsf, ngw_raw = e.ngw;
-#else
-#pragma unroll 1
-    for (int j = 0; j < 3; j++) {
+    for (int j = 0; j < (is_lake ? 0 : 3); j++) {     // lake elements: fun_Ele_lakeHorizon, all zero
         const int nb = j == 0 ? mt.x : j == 1 ? mt.y : mt.z;
         const double2 g = ldnt2(&p.ged[(size_t)j * NEl + i]);
         const int nc = nb >= 0 ? nb : i;                  // boundary edge: harmless in-bounds loads
         const double2 nzz = p.zz[nc];
         const int ncf = p.meta[nc].w;
         const double nsf_raw = Y.sf(nc), ngw_raw = Y.gw(nc);
-#endif
         const double B = g.x, d2n = g.y;
         double qsf = 0., qsb = 0.;
-        if (nb >= 0) {
-            const int cn = cf_class(ncf);
+        const int cn = cf_class(ncf);
 #define CN(f) (LCT ? lct[cn * CF_LDS_STRIDE + CF_##f] : p.ctab[CF_##f * ncls + cn])
+        if (LAKE && nb >= 0 && ncf < 0) {                 // bank edge: the neighbour is a lake element
+            const int l = lk.lake_of[nb];
+            const double zl = lk.bathy_y[lk.bathy_off[l]];               // lake[l].zmin = bathymetry.yi[0]
+            const double yl = Y.y[lk.y_off + l];                         // yLakeStg (serial: unclamped)
+            const double nsf = yl < 0. ? 0. : yl;
+            qsf = weir_jtoi(zl, nsf, zs, isf, zs, 0.6, B, 0.01);          // MD_ElementFlux.cpp:46-53
+            const double dhg = (ugw + zb) - (yl + zl);                   // MD_ElementFlux.cpp:107-121
+            double q = 0.;
+            if (dhg > 0. && ugw <= 0.02) q = 0.;
+            else if (dhg < 0. && yl <= 0.02) q = 0.;
+            else {
+                const double ymg = (rmax(ugw, 0.) + rmax(yl, 0.)) * .5;
+                const double grad = SDIV(dhg, d2n);
+                const double kmean = 0.5 * (ekh + CN(KsatH));            // the lake element's u_effKH = KsatH
+                q = kmean * grad * ymg * B;
+            }
+            lk.bank_qs[(size_t)j * NEl + i] = qsf;
+            lk.bank_qg[(size_t)j * NEl + i] = q;
+            qsb = q * fu_sub;
+        } else if (nb >= 0) {
             double nsf = nsf_raw;
             if (MODE == 1) nsf = (nsf >= 0.) ? nsf : 0.;
             nsf = nsf < 0. ? 0. : nsf;
@@ -322,7 +297,6 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
             else if (dhg < 0. && ugn <= 0.02) q = 0.;
             else {
                 const double ekn = eff_kh(ugn, zsn - zbn, CN(macD), CN(macKsatH), CN(vAreaF), CN(KsatH));
-#undef CN
                 const double ymg = (rmax(ugw, 0.) + rmax(ugn, 0.)) * .5;
                 const double grad = SDIV(dhg, d2n);
                 const double kmean = 0.5 * (ekh + ekn);
@@ -344,14 +318,17 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
             }
             qsb = q * fu_sub;
         }
+#undef CN
         if (MODE == 0) nan_q |= (isnan(qsf) || isinf(qsf) || isnan(qsb) || isinf(qsb));
         sumsurf += qsf;
         sumsub += qsb;
         if (DIAG) { dg.qele_surf[j * NEl + i] = qsf; dg.qele_sub[j * NEl + i] = qsb; }
     }
+    if (DIAG && is_lake)
+        for (int j = 0; j < 3; j++) { dg.qele_surf[j * NEl + i] = 0.; dg.qele_sub[j * NEl + i] = 0.; }
     if (MODE == 0) report_w(m.err, nan_q, 0x01u, 0, i);       // CheckNANij, MD_f.cpp:73-74
 
-    // ---- f_applyDY element part (MD_f.cpp:88-131 / MD_f_omp.cpp:26-46) ----
+    // ---- f_applyDY element part (MD_f.cpp:88-150 / MD_f_omp.cpp:26-46) ----
     const double area = ldnt(&p.area[i]);
     double dsf = dsf_head - SDIV(sumsurf, area) - Es;
     double dgw = dgw_head - SDIV(sumsub, area) - Eg - Tg;
@@ -360,6 +337,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     if (iss == 1) dsf += 0.0 / area;                          // QSS is never assigned: 0
     else if (iss == 2) dgw += 0.0 / area;
     dgw = CDIV(dgw, Sy);
+    if (is_lake) { dsf = 0.; dgw = 0.; }                      // MD_f.cpp:146-150
 #undef CL
     __builtin_nontemporal_store(dsf, &dy[i]);
     __builtin_nontemporal_store(dgw, &dy[2 * nown + i]);
@@ -494,6 +472,91 @@ void launch_river_kernel_packed(const DevMesh &m, const DevPacked &p, const YVie
     }
 }
 
+// ===================================================================================
+// lakes: one workgroup per lake.  Every lake sum keeps the reference's order — lake elements
+// ascending (MD_f.cpp:16-17), bank edges by element then edge (MD_ElementFlux.cpp:52,121), inflowing reaches
+// ascending (MD_RiverFlux.cpp:24) — by staging each 256-wide chunk of terms in LDS (parallel loads) and
+// adding them on one lane.  A lake has O(1e3) terms: the kernel is latency-bound and tiny.
+// ===================================================================================
+// Lake.cpp:59-79 LakeBathymetry::toparea, the reference's own interpolation as written
+__device__ double lake_toparea(const DevLake &L, int l, double y) {
+    const double *yi = L.bathy_y + L.bathy_off[l], *ai = L.bathy_a + L.bathy_off[l];
+    const int nvalue = L.bathy_off[l + 1] - L.bathy_off[l];
+    double ta = ai[0];
+    if (y <= yi[0]) {
+        ta = ai[0];
+    } else {
+        for (int k = 1; k < nvalue; k++) {
+            if (y < yi[k]) {
+                const double da = (ai[k] - ta), dyy = yi[k] - y;
+                ta = da / dyy * (y - yi[k - 1]) + ta;
+                break;
+            }
+            ta = ai[k];
+        }
+    }
+    return ta;
+}
+
+// ordered sum of f(k) for k in [k0, k1): chunks of blockDim.x loaded in parallel, added in order by lane 0
+template <class F>
+__device__ double ordered_sum(int k0, int k1, F f, double *buf) {
+    double acc = 0.;
+    for (int b = k0; b < k1; b += blockDim.x) {
+        const int k = b + (int)threadIdx.x;
+        if (k < k1) buf[threadIdx.x] = f(k);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int n = min((int)blockDim.x, k1 - b);
+            for (int t = 0; t < n; t++) acc += buf[t];
+        }
+        __syncthreads();
+    }
+    return acc;                                  // valid on lane 0
+}
+
+__global__ void __launch_bounds__(256)
+shud_lake_kernel(DevMesh m, DevPacked p, DevLake L, YView Y, double *__restrict__ dy, int diag, DevDiag dg) {
+    __shared__ double buf[256];
+    const int l = blockIdx.x;
+    const double yl = Y.y[L.y_off + l];                                   // yLakeStg (MD_update.cpp:175)
+    const int e0 = L.ele_off[l], e1 = L.ele_off[l + 1];
+    const double n_ele = (double)(e1 - e0);                               // lake[l].NumEleLake
+    // qLakeEvap += qEleEvapo / NumEleLake (qEleEvapo = qPotEvap, fun_Ele_lakeVertical); qLakePrcp likewise
+    const double qevap = ordered_sum(e0, e1, [&](int k) { return m.pot_evap[L.ele_idx[k]] / n_ele; }, buf);
+    const double qprcp = ordered_sum(e0, e1, [&](int k) { return m.prcp[L.ele_idx[k]] / n_ele; }, buf);
+    const double qsurf = ordered_sum(L.bank_off[l], L.bank_off[l + 1],
+                                     [&](int k) { return L.bank_qs[L.bank_pos[k]]; }, buf);
+    const double qsub = ordered_sum(L.bank_off[l], L.bank_off[l + 1],
+                                    [&](int k) { return L.bank_qg[L.bank_pos[k]]; }, buf);
+    // QLakeRivIn += QrivDown of each inflowing reach (zero-depth-gradient Manning, MD_RiverFlux.cpp:17-25),
+    // recomputed here from the reach's own stage with the river kernel's functions
+    const double qin = ordered_sum(L.rin_off[l], L.rin_off[l + 1], [&](int k) {
+        const int r = L.rin_idx[k];
+        const RivP q = riv_load(p, r);
+        double yg;
+        const double ur = riv_stage_p<0>(m, Y, r, q.bc, &yg);
+        return riv_down_p(q, ur, riv_geom_p(q, yg), 0., 0., 0.);          // q.down = -3: outlet formula
+    }, buf);
+    if (threadIdx.x == 0) {
+        const double zmin = L.bathy_y[L.bathy_off[l]];
+        const double area = lake_toparea(L, l, yl + zmin);                // _Lake::update (Lake.cpp:104-107)
+        double qe = rmin(qevap, qprcp + yl);                              // MD_f.cpp:44-47
+        qe = rmax(0, qe);
+        dy[L.y_off + l] = qprcp - qe + (qin - 0. + qsub + qsurf) / area;  // MD_f.cpp:180-183 (QLakeRivOut = 0)
+        if (diag) {
+            dg.q_lake_surf[l] = qsurf; dg.q_lake_sub[l] = qsub; dg.q_lake_rivin[l] = qin;
+            dg.q_lake_evap[l] = qe; dg.q_lake_prcp[l] = qprcp; dg.lake_toparea[l] = area;
+        }
+    }
+}
+
+void launch_lake_kernel(const DevMesh &m, const DevPacked &p, const DevLake &L, const YView &Y, double *dy,
+                        bool diag, const DevDiag &dg, hipStream_t s) {
+    if (L.nl <= 0) return;
+    hipLaunchKernelGGL(shud_lake_kernel, dim3(L.nl), dim3(256), 0, s, m, p, L, Y, dy, diag ? 1 : 0, dg);
+}
+
 // step inputs (SoA staging in DevMesh) -> packed records; `what` bits: 1 np, 2 tl, 4 fu, 8 u_satn, 16 e_ic
 __global__ void __launch_bounds__(256)
 shud_pack_step_kernel(DevMesh m, DevPacked p, int n, int cur, unsigned what) {
@@ -506,22 +569,27 @@ shud_pack_step_kernel(DevMesh m, DevPacked p, int n, int cur, unsigned what) {
     if (what & 16) p.cs[cur][i].y = m.e_ic[0][i];
 }
 
-template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT>
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE>
 static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1, int cur,
-                     const DevDiag &dg, hipStream_t s) {
+                     const DevDiag &dg, const DevLake &lk, hipStream_t s) {
     int nb = (i1 - i0 + 255) / 256;
     nb = (nb + 7) / 8 * 8;                  // block_id<1> deals blocks to XCDs in contiguous chunks
     const size_t lds = LCT ? (size_t)p.ncls * CF_LDS_STRIDE * sizeof(double) : 0;
-    hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT>), dim3(nb), dim3(256), lds, s, m, p, Y, dy,
-                       i0, i1, cur, dg);
+    hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT, LAKE>), dim3(nb), dim3(256), lds, s, m, p,
+                       Y, dy, i0, i1, cur, dg, lk);
 }
 
 void launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1,
                                   int cur, int mode, bool open, bool diag, bool fu_unit, const DevDiag &dg,
-                                  hipStream_t s) {
+                                  hipStream_t s, const DevLake *lake) {
     if (i1 <= i0) return;
-#define LP(MO, OP, DI, FU) do { if (p.ncls <= LDS_CLS_MAX) launch_p<MO, OP, DI, FU, true>(m, p, Y, dy, i0, i1, cur, dg, s); \
-                                 else launch_p<MO, OP, DI, FU, false>(m, p, Y, dy, i0, i1, cur, dg, s); } while (0)
+    DevLake lk{};
+    if (lake) lk = *lake;
+    // lakes: serial semantics only (the handle rejects OMP + lakes), class table in LDS
+#define LP(MO, OP, DI, FU) do {                                                                            \
+        if (lake && MO == 0) launch_p<MO, OP, DI, FU, true, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s);    \
+        else if (p.ncls <= LDS_CLS_MAX) launch_p<MO, OP, DI, FU, true, false>(m, p, Y, dy, i0, i1, cur, dg, lk, s); \
+        else launch_p<MO, OP, DI, FU, false, false>(m, p, Y, dy, i0, i1, cur, dg, lk, s); } while (0)
 #define LFU(MO, OP, DI) do { if (fu_unit) LP(MO, OP, DI, true); else LP(MO, OP, DI, false); } while (0)
 #define LDI(MO, OP) do { if (diag) LFU(MO, OP, true); else LFU(MO, OP, false); } while (0)
 #define LOP(MO) do { if (open) LDI(MO, true); else LDI(MO, false); } while (0)

@@ -79,7 +79,7 @@ extern "C" int shud_et_attach(shud_rhs_t h, const ShudEtMeshSoA *m, const ShudEt
     e.iforc = iforc; e.ilc = ilc; e.imf = imf; e.ilake = ilake;
     e.z_surf = dz; e.albedo = dalb; e.fixp = dfp; e.windh = dwh; e.vegf = dvf; e.nx = dnx; e.ny = dny; e.nz = dnz;
     double **state[] = {&e.y_is, &e.y_snow, &e.tsr_factor, &e.tacc_surf, &e.tacc_sub, &e.acc_surf, &e.acc_sub,
-                        &e.t_prcp, &e.t_temp, &e.t_mf, &e.t_rn, &e.t_wind, &e.t_rh, &e.rn_factor, &e.q_prep};
+                        &e.t_prcp, &e.t_temp, &e.t_mf, &e.t_rn, &e.t_wind, &e.t_rh, &e.rn_factor};
     for (double **q : state)
         if ((rc = h->upload(q, (const double *)nullptr, NE))) return rc;   // zero: ACC starts at 0 (see DESIGN)
     if (p->cryosphere) {
@@ -98,6 +98,7 @@ extern "C" int shud_et_attach(shud_rhs_t h, const ShudEtMeshSoA *m, const ShudEt
     e.q_netp = const_cast<double *>(h->dm.net_prep);
     e.fu_surf = const_cast<double *>(h->dm.fu_surf);
     e.fu_sub = const_cast<double *>(h->dm.fu_sub);
+    e.q_prep = const_cast<double *>(h->dm.prcp);           // qElePrep: lake elements' precipitation
     return SHUD_OK;
 }
 

@@ -35,6 +35,9 @@ struct EtState;                           // shud_et.cpp
 struct shud_rhs {
     int NE = 0, NR = 0, NS = 0;          // local totals (incl. ghosts)
     int n_own = 0, n_segghost = 0, n_own_riv = 0;
+    bool lakeon = false;                 // lakes: any iLake > 0; serial, unpartitioned, packed
+    int NL = 0;
+    DevLake lk{};
     int n_int = 0;                       // partitioned: owned prefix independent of ghost data
     int mode = SHUD_MODE_SERIAL;
     bool open = false;

@@ -61,6 +61,7 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
                         const std::vector<int> &seg_off, const std::vector<int> &up_off,
                         const std::vector<int> &up_idx);
 
+static int build_lakes(shud_rhs *h, const ShudMeshSoA *m);
 static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, const ShudRhsOptions *opt,
                  const ShudPartition *part) {
     const int NE = m->num_ele, NR = m->num_riv, NS = m->num_seg;
@@ -93,14 +94,38 @@ static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, cons
         if (!pp[k]) return shud_fail(SHUD_ERR_ARG, "missing parameter array #%d", k);
     for (long long q = 0; q < 3LL * NE; q++)
         if (m->nabr[q] < -1 || m->nabr[q] >= NE) return shud_fail(SHUD_ERR_ARG, "nabr[%lld]=%d out of range", q, m->nabr[q]);
+    // lakes: on when any iLake > 0 (MD_readin.cpp:262-263); serial semantics, unpartitioned, packed layout
     if (m->ilake)
         for (int i = 0; i < NE; i++)
-            if (m->ilake[i] > 0) return shud_fail(SHUD_ERR_UNSUPPORTED, "lake element %d: lake module not supported", i);
+            if (m->ilake[i] > 0) h->lakeon = true;
+    if (h->lakeon) {
+        if (h->mode != SHUD_MODE_SERIAL)
+            return shud_fail(SHUD_ERR_UNSUPPORTED, "lakes: the OMP path has no lake physics (MD_f_omp.cpp)");
+        if (part) return shud_fail(SHUD_ERR_UNSUPPORTED, "lakes: partitioned handles not supported");
+        h->NL = m->num_lake;
+        if (h->NL <= 0 || !m->lake_bathy_off || !m->lake_bathy_y || !m->lake_bathy_a)
+            return shud_fail(SHUD_ERR_ARG, "lake elements present but no lake bathymetry (num_lake %d)", m->num_lake);
+        for (int l = 0; l < h->NL; l++)
+            if (m->lake_bathy_off[l + 1] <= m->lake_bathy_off[l])
+                return shud_fail(SHUD_ERR_ARG, "lake %d has an empty bathymetry table", l + 1);
+        for (int i = 0; i < NE; i++)
+            if (m->ilake[i] > h->NL) return shud_fail(SHUD_ERR_ARG, "element %d: iLake %d > num_lake", i, m->ilake[i]);
+    }
     for (int r = 0; r < NR; r++) {
         int d = m->riv_down[r];
+        if (h->lakeon && d <= -4) {               // toLake = (-3 - down) - 1 (MD_Lake.cpp:46-50)
+            if ((-3 - d) - 1 >= h->NL)
+                return shud_fail(SHUD_ERR_ARG, "reach %d flows into lake %d > num_lake", r, -3 - d);
+            continue;
+        }
         if (d >= NR || (d < 0 && d < -4))
             return shud_fail(SHUD_ERR_ARG, "Fatal Error: River Routing Boundary Condition Type Is Wrong! (reach %d down %d)", r, d);
     }
+    // reach codes as the kernels see them: a reach into a lake uses the zero-depth-gradient formula (-3)
+    std::vector<int> rdown(m->riv_down, m->riv_down + NR);
+    if (h->lakeon)
+        for (int r = 0; r < NR; r++)
+            if (rdown[r] <= -4) rdown[r] = -3;
     for (int s = 0; s < NS; s++)
         if (m->seg_ele[s] < 0 || m->seg_ele[s] >= NE || m->seg_riv[s] < 0 || m->seg_riv[s] >= NR)
             return shud_fail(SHUD_ERR_ARG, "segment %d references element/reach out of range", s);
@@ -226,7 +251,8 @@ static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, cons
         UP(Sy, p->Sy, NE); UP(RzD, p->RzD, NE); UP(VegFrac, p->VegFrac, NE); UP(ImpAF, p->ImpAF, NE);
     }
     {
-        double *net_prep_w, *pot_evap_w, *pot_tran_w, *etp_w, *lai_w, *fu_surf_w, *fu_sub_w, *ugw_stale_w;
+        double *net_prep_w, *pot_evap_w, *pot_tran_w, *etp_w, *lai_w, *fu_surf_w, *fu_sub_w, *ugw_stale_w, *prcp_w;
+        UP(prcp, (const double *)nullptr, NE);
         UP(net_prep, (const double *)nullptr, NE); UP(pot_evap, (const double *)nullptr, NE); UP(pot_tran, (const double *)nullptr, NE); UP(etp, (const double *)nullptr, NE);
         UP(lai, (const double *)nullptr, NE);
         if ((rc = h->upload_fill(&fu_surf_w, (const double *)nullptr, NE, 1.0))) return rc;
@@ -258,7 +284,7 @@ static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, cons
         int *riv_down_w, *riv_bc_w, *up_off_w, *up_idx_w, *rseg_off_w, *rseg_pos_w;
         double *riv_len_w, *riv_slope_w, *riv_d2down_w, *riv_avg_rough_w, *riv_depth_w, *riv_bw_w,
             *riv_bankslope_w, *riv_ksath_w, *riv_bedthick_w;
-        UP(riv_down, m->riv_down, NR); UP(riv_bc, rbc.data(), NR);
+        UP(riv_down, rdown.data(), NR); UP(riv_bc, rbc.data(), NR);
         UP(riv_len, m->riv_length, NR); UP(riv_slope, m->riv_bed_slope, NR); UP(riv_d2down, m->riv_dist2down, NR);
         UP(riv_avg_rough, m->riv_avg_rough, NR); UP(riv_depth, m->riv_depth, NR); UP(riv_bw, m->riv_bottom_width, NR);
         UP(riv_bankslope, m->riv_bankslope, NR); UP(riv_ksath, m->riv_ksath, NR); UP(riv_bedthick, m->riv_bedthick, NR);
@@ -267,11 +293,12 @@ static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, cons
     }
 #undef UP
     if ((rc = build_packed(h, m, p, eflags, seg_off, up_off, up_idx))) return rc;
+    if (h->lakeon && (rc = build_lakes(h, m))) return rc;
     if ((rc = h->dalloc(&h->d_err, 1))) return rc;
     d.err = h->d_err;
     HIP_TRY(hipHostMalloc((void **)&h->h_err, sizeof(DevErr), hipHostMallocDefault));
     if ((rc = shud_reset_err(h))) return rc;
-    const size_t ny = 3 * (size_t)h->n_own + h->n_own_riv;
+    const size_t ny = 3 * (size_t)h->n_own + h->n_own_riv + h->NL;
     if ((rc = h->dalloc(&h->d_y, ny))) return rc;
     if ((rc = h->dalloc(&h->d_ydot, ny))) return rc;
     if ((rc = h->dalloc(&h->d_scratch_dy, ny))) return rc;
@@ -319,7 +346,7 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         std::string k((const char *)r.data(), r.size() * sizeof(double));
         auto it = ids.find(k);
         if (it == ids.end()) {
-            if ((int)table.size() >= 65536) return 0;
+            if ((int)table.size() >= 32768) return 0;
             it = ids.emplace(k, (int)table.size()).first;
             table.push_back(r);
         }
@@ -354,8 +381,9 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         zz[i] = make_double2(m->z_surf[i], m->z_bottom[i]);
         const int nseg = seg_off[i + 1] - seg_off[i];
         const int ibc = (int8_t)(eflags[i] & 0xff);
+        const bool lake_ele = m->ilake && m->ilake[i] > 0 && h->lakeon;
         const unsigned cf = (unsigned)(ibc & 0xff) | ((unsigned)((eflags[i] >> 16) & 3) << 8) |
-                            ((unsigned)nseg << 10) | ((unsigned)cls[i] << 16);
+                            ((unsigned)nseg << 10) | ((unsigned)cls[i] << 16) | (lake_ele ? 0x80000000u : 0u);
         meta[i] = make_int4(m->nabr[i], m->nabr[(size_t)NE + i], m->nabr[2 * (size_t)NE + i], (int)cf);
         for (int j = 0; j < 3; j++)
             ged[(size_t)j * NE + i] = make_double2(m->edge[(size_t)j * NE + i], m->dist2nabor[(size_t)j * NE + i]);
@@ -415,7 +443,8 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         rb[r] = make_double2(m->riv_length[r], m->riv_bed_slope[r]);
         rcc[r] = make_double2(m->riv_dist2down[r], m->riv_avg_rough[r]);
         rd[r] = make_double2(m->riv_depth[r], 0.0);
-        ri[r] = make_int4(m->riv_down[r], m->riv_bc ? m->riv_bc[r] : 0, rstart[r], rcnt[r]);
+        const int dn = (h->lakeon && m->riv_down[r] <= -4) ? -3 : m->riv_down[r];   // into a lake: outlet formula
+        ri[r] = make_int4(dn, m->riv_bc ? m->riv_bc[r] : 0, rstart[r], rcnt[r]);
         int4 u = make_int4(0, 0, 0, 0);
         if (r < nor) {
             const int n = up_off[r + 1] - up_off[r];
@@ -439,6 +468,62 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     P.rv_a = ra_d; P.rv_b = rb_d; P.rv_c = rc_d; P.rv_d = rd_d; P.rv_i = ri_d; P.rv_u = ru_d;
     h->n_classes = ncls;
     h->packed = true;
+    return 0;
+}
+
+// Lakes: lake / bank-edge / inflow lists in the reference's summation orders, bathymetry.
+static int build_lakes(shud_rhs *h, const ShudMeshSoA *m) {
+    const int NE = m->num_ele, NR = m->num_riv, NL = h->NL;
+    if (!h->packed || h->variant)
+        return shud_fail(SHUD_ERR_UNSUPPORTED, "lakes need the packed layout (mesh did not qualify or SHUD_RHS_PACKED=0)");
+    if (h->n_classes > 128) return shud_fail(SHUD_ERR_UNSUPPORTED, "lakes: more than 128 parameter classes");
+    std::vector<int> lake_of(NE, -1), ele_off(NL + 1, 0), bank_off(NL + 1, 0), rin_off(NL + 1, 0);
+    std::vector<int> ele_idx, bank_pos, rin_idx;
+    for (int i = 0; i < NE; i++)
+        if (m->ilake[i] > 0) { lake_of[i] = m->ilake[i] - 1; ele_off[m->ilake[i]]++; }
+    // bank edges: a non-lake element's edge whose neighbour is a lake element (lakenabr, MD_Lake.cpp:131-143)
+    auto bank_lake = [&](int i, int j) -> int {
+        if (m->ilake[i] > 0) return -1;
+        const int nb = m->nabr[(size_t)j * NE + i];
+        return (nb >= 0 && m->ilake[nb] > 0) ? m->ilake[nb] - 1 : -1;
+    };
+    for (int i = 0; i < NE; i++)
+        for (int j = 0; j < 3; j++) { const int l = bank_lake(i, j); if (l >= 0) bank_off[l + 1]++; }
+    for (int r = 0; r < NR; r++)
+        if (m->riv_down[r] <= -4) rin_off[(-3 - m->riv_down[r])]++;
+    for (int l = 0; l < NL; l++) {
+        ele_off[l + 1] += ele_off[l]; bank_off[l + 1] += bank_off[l]; rin_off[l + 1] += rin_off[l];
+    }
+    ele_idx.resize(ele_off[NL]); bank_pos.resize(bank_off[NL]); rin_idx.resize(rin_off[NL]);
+    {
+        std::vector<int> fe(ele_off.begin(), ele_off.end() - 1), fb(bank_off.begin(), bank_off.end() - 1),
+            fr(rin_off.begin(), rin_off.end() - 1);
+        for (int i = 0; i < NE; i++) {                  // ascending element, then edge: the reference's order
+            if (m->ilake[i] > 0) ele_idx[fe[m->ilake[i] - 1]++] = i;
+            for (int j = 0; j < 3; j++) { const int l = bank_lake(i, j); if (l >= 0) bank_pos[fb[l]++] = j * NE + i; }
+        }
+        for (int r = 0; r < NR; r++)
+            if (m->riv_down[r] <= -4) { const int l = (-3 - m->riv_down[r]) - 1; rin_idx[fr[l]++] = r; }
+    }
+    for (int l = 0; l < NL; l++)
+        if (ele_off[l + 1] == ele_off[l]) return shud_fail(SHUD_ERR_ARG, "lake %d has no lake element", l + 1);
+    DevLake &L = h->lk;
+    L.nl = NL;
+    L.y_off = 3 * NE + NR;
+    int rc;
+    int *lo, *eo, *ei, *bo, *bp, *ro, *ri, *bto;
+    double *by, *ba;
+    const int nb = m->lake_bathy_off[NL];
+    if ((rc = h->upload(&lo, lake_of.data(), NE)) || (rc = h->upload(&eo, ele_off.data(), NL + 1)) ||
+        (rc = h->upload(&ei, ele_idx.data(), ele_idx.size())) || (rc = h->upload(&bo, bank_off.data(), NL + 1)) ||
+        (rc = h->upload(&bp, bank_pos.data(), bank_pos.size())) || (rc = h->upload(&ro, rin_off.data(), NL + 1)) ||
+        (rc = h->upload(&ri, rin_idx.data(), rin_idx.size())) || (rc = h->upload(&bto, m->lake_bathy_off, NL + 1)) ||
+        (rc = h->upload(&by, m->lake_bathy_y, nb)) || (rc = h->upload(&ba, m->lake_bathy_a, nb)) ||
+        (rc = h->upload(&L.bank_qs, (const double *)nullptr, 3 * (size_t)NE)) ||
+        (rc = h->upload(&L.bank_qg, (const double *)nullptr, 3 * (size_t)NE)))
+        return rc;
+    L.lake_of = lo; L.ele_off = eo; L.ele_idx = ei; L.bank_off = bo; L.bank_pos = bp; L.rin_off = ro; L.rin_idx = ri;
+    L.bathy_off = bto; L.bathy_y = by; L.bathy_a = ba;
     return 0;
 }
 
@@ -545,7 +630,7 @@ extern "C" int shud_rhs_set_step_inputs(shud_rhs_t h, const ShudStepInputs *in) 
     struct { const double *src; const double *dst; } arr[] = {
         {in->net_prep, h->dm.net_prep}, {in->pot_evap, h->dm.pot_evap}, {in->pot_tran, h->dm.pot_tran},
         {in->etp, h->dm.etp}, {in->lai, h->dm.lai}, {in->fu_surf, h->dm.fu_surf}, {in->fu_sub, h->dm.fu_sub},
-        {in->ugw_stale, h->dm.ugw_stale}, {in->e_ic, eic_dst}, {in->u_satn, satn_dst}};
+        {in->ugw_stale, h->dm.ugw_stale}, {in->e_ic, eic_dst}, {in->u_satn, satn_dst}, {in->prcp, h->dm.prcp}};
     for (auto &a : arr)
         if (a.src) HIP_TRY(hipMemcpyAsync((void *)a.dst, a.src, nb, hipMemcpyHostToDevice, h->stream));
     if (h->packed) {
@@ -612,7 +697,7 @@ static void launch_ele(shud_rhs *h, const double *y, double *dy, int cur, int cu
     if (i1 < 0) i1 = h->n_own + h->n_segghost;
     if (h->packed && !h->variant)
         launch_element_kernel_packed(h->dm, h->dp, Y, dy, i0, i1, cur, h->mode, h->open, diag,
-                                     h->fu_unit[0] && h->fu_unit[1], h->dd, h->stream);
+                                     h->fu_unit[0] && h->fu_unit[1], h->dd, h->stream, h->lakeon ? &h->lk : nullptr);
     else
         launch_element_kernel(h->dm, Y, dy, h->n_own + h->n_segghost, cur, cur_e, h->mode, h->open, diag, h->dd,
                               h->stream, h->variant);
@@ -623,6 +708,7 @@ static void launch_riv(shud_rhs *h, const double *y, double *dy, bool diag) {
         launch_river_kernel_packed(h->dm, h->dp, Y, dy, h->mode, diag, h->dd, h->stream);
     else
         launch_river_kernel(h->dm, Y, dy, h->mode, diag, h->dd, h->stream);
+    if (h->lakeon) launch_lake_kernel(h->dm, h->dp, h->lk, Y, dy, diag, h->dd, h->stream);
 }
 static void launch_all(shud_rhs *h, const double *y, double *dy, int cur, int cur_e, bool diag) {
     launch_ele(h, y, dy, cur, cur_e, diag);
@@ -675,7 +761,7 @@ static int eval_device(shud_rhs *h, double t, const double *y, double *dy) {
 
 extern "C" int shud_rhs_eval(shud_rhs_t h, double t, const double *y, double *ydot, int where) {
     if (!h || !y || !ydot) return shud_fail(SHUD_ERR_ARG, "null argument");
-    const size_t ny = 3 * (size_t)h->n_own + h->n_own_riv;
+    const size_t ny = 3 * (size_t)h->n_own + h->n_own_riv + h->NL;
     if (where == SHUD_WHERE_DEVICE) return eval_device(h, t, y, ydot);
     if (where != SHUD_WHERE_HOST) return shud_fail(SHUD_ERR_ARG, "bad where");
     HIP_TRY(hipSetDevice(h->device));
@@ -786,6 +872,10 @@ static int ensure_diag(shud_rhs *h) {
     double **r1[] = {&h->dd.qriv_down, &h->dd.qriv_up, &h->dd.qriv_surf, &h->dd.qriv_sub};
     for (auto pp : r1)
         if ((rc = h->upload(pp, (const double *)nullptr, NR))) return rc;
+    double **l1[] = {&h->dd.q_lake_surf, &h->dd.q_lake_sub, &h->dd.q_lake_rivin, &h->dd.q_lake_evap,
+                     &h->dd.q_lake_prcp, &h->dd.lake_toparea};
+    for (auto pp : l1)
+        if ((rc = h->upload(pp, (const double *)nullptr, std::max(h->NL, 1)))) return rc;
     h->have_diag = true;
     return 0;
 }
@@ -815,7 +905,10 @@ extern "C" int shud_rhs_sync_diagnostics(shud_rhs_t h, ShudFluxOut *o) {
         (rc = get(o->eff_kh, g.eff_kh, NE)) || (rc = get(o->qe2r_surf, g.qe2r_surf, NE)) ||
         (rc = get(o->qe2r_sub, g.qe2r_sub, NE)) || (rc = get(o->qriv_down, g.qriv_down, NR)) ||
         (rc = get(o->qriv_up, g.qriv_up, NR)) || (rc = get(o->qriv_surf, g.qriv_surf, NR)) ||
-        (rc = get(o->qriv_sub, g.qriv_sub, NR)))
+        (rc = get(o->qriv_sub, g.qriv_sub, NR)) || (rc = get(o->q_lake_surf, g.q_lake_surf, h->NL)) ||
+        (rc = get(o->q_lake_sub, g.q_lake_sub, h->NL)) || (rc = get(o->q_lake_rivin, g.q_lake_rivin, h->NL)) ||
+        (rc = get(o->q_lake_evap, g.q_lake_evap, h->NL)) || (rc = get(o->q_lake_prcp, g.q_lake_prcp, h->NL)) ||
+        (rc = get(o->lake_toparea, g.lake_toparea, h->NL)))
         return rc;
     std::vector<double> tmp;
     if (o->qseg_surf || o->qseg_sub) tmp.resize(std::max<size_t>(NS, 1));

@@ -39,6 +39,8 @@ MESH_FIELDS = [
     ("riv_bottom_width", c_double_p), ("riv_bankslope", c_double_p), ("riv_ksath", c_double_p),
     ("riv_bedthick", c_double_p),
     ("seg_ele", c_int32_p), ("seg_riv", c_int32_p), ("seg_length", c_double_p), ("seg_cwr", c_double_p),
+    ("num_lake", C.c_int32), ("lake_bathy_off", c_int32_p), ("lake_bathy_y", c_double_p),
+    ("lake_bathy_a", c_double_p),
 ]
 PARAM_NAMES = ["aquifer_depth", "macD", "macKsatH", "geo_vAreaF", "KsatH", "KsatV", "infKsatV", "hAreaF",
                "macKsatV", "ThetaS", "ThetaR", "Beta", "infD", "Sy", "RzD", "VegFrac", "ImpAF"]
@@ -49,6 +51,7 @@ DIAG_ELE = ["qele_surf_tot", "qele_sub_tot", "q_infil", "q_exfil", "q_recharge",
             "q_tu", "q_tg", "q_eta", "e_ic", "u_satn", "i_beta", "eff_kh", "qe2r_surf", "qe2r_sub"]
 DIAG_SEG = ["qseg_surf", "qseg_sub"]
 DIAG_RIV = ["qriv_down", "qriv_up", "qriv_surf", "qriv_sub"]
+DIAG_LAKE = ["q_lake_surf", "q_lake_sub", "q_lake_rivin", "q_lake_evap", "q_lake_prcp", "lake_toparea"]
 
 
 class ShudMeshSoA(C.Structure):
@@ -65,6 +68,7 @@ class ShudStepInputs(C.Structure):
         ("ele_qbc", c_double_p), ("n_ele_qbc", C.c_int32),
         ("riv_ybc", c_double_p), ("n_riv_ybc", C.c_int32),
         ("riv_qbc", c_double_p), ("n_riv_qbc", C.c_int32),
+        ("prcp", c_double_p),
     ]
 
 
@@ -78,7 +82,8 @@ class ShudFluxOut(C.Structure):
                                                                         "q_eta", "e_ic", "u_satn", "i_beta",
                                                                         "eff_kh", "qe2r_surf", "qe2r_sub",
                                                                         "qseg_surf", "qseg_sub", "qriv_down",
-                                                                        "qriv_up", "qriv_surf", "qriv_sub"]]
+                                                                        "qriv_up", "qriv_surf", "qriv_sub"]
+                                                                      + DIAG_LAKE]
 
 
 FLUXOUT_ORDER = [f[0] for f in ShudFluxOut._fields_]

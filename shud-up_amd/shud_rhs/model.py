@@ -55,10 +55,15 @@ class ShudModel:
     step: Dict[str, np.ndarray] = field(default_factory=dict)    # abi.STEP_ARRAYS [NE]
     bc_tables: Dict[str, np.ndarray] = field(default_factory=dict)  # ele_ybc, ele_qbc, riv_ybc, riv_qbc
     meta: Dict[str, object] = field(default_factory=dict)
+    # lakes: bathymetry table per lake, rows [off[l], off[l+1])
+    num_lake: int = 0
+    lake_bathy_off: Optional[np.ndarray] = None
+    lake_bathy_y: Optional[np.ndarray] = None
+    lake_bathy_a: Optional[np.ndarray] = None
 
     @property
     def num_y(self):
-        return 3 * self.num_ele + self.num_riv
+        return 3 * self.num_ele + self.num_riv + self.num_lake
 
     def finalize(self):
         """Coerce dtypes / contiguity and fill defaults; returns self."""
@@ -90,6 +95,10 @@ class ShudModel:
             self.step[k] = _d(self.step[k])
         for k in list(self.bc_tables):
             self.bc_tables[k] = _d(self.bc_tables[k])
+        if self.num_lake:
+            self.lake_bathy_off = _i(self.lake_bathy_off)
+            self.lake_bathy_y = _d(self.lake_bathy_y)
+            self.lake_bathy_a = _d(self.lake_bathy_a)
         return self
 
     # ---- C structs (the returned struct references arrays owned by self) ----
@@ -110,6 +119,10 @@ class ShudModel:
         m.seg_riv = _ptr(self.seg_riv, C.c_int32)
         m.seg_length = _ptr(self.seg_length, C.c_double)
         m.seg_cwr = _ptr(self.seg_cwr, C.c_double)
+        m.num_lake = self.num_lake
+        m.lake_bathy_off = _ptr(self.lake_bathy_off if self.num_lake else None, C.c_int32)
+        m.lake_bathy_y = _ptr(self.lake_bathy_y if self.num_lake else None, C.c_double)
+        m.lake_bathy_a = _ptr(self.lake_bathy_a if self.num_lake else None, C.c_double)
         return m
 
     def params_struct(self):
@@ -140,6 +153,11 @@ class ShudModel:
             else:
                 setattr(s, k, _ptr(None, C.c_double))
                 setattr(s, "n_" + k, 0)
+        a = step.get("prcp")
+        if a is not None:
+            a = _d(a)
+            keep.append(a)
+        s.prcp = _ptr(a, C.c_double)
         s._keep = keep
         return s
 
@@ -160,6 +178,9 @@ class ShudModel:
             d[k] = getattr(self, k)
         if self.ilake is not None:
             d["ilake"] = self.ilake
+        if self.num_lake:
+            d["lake_bathy_off"], d["lake_bathy_y"], d["lake_bathy_a"] = (self.lake_bathy_off, self.lake_bathy_y,
+                                                                        self.lake_bathy_a)
         np.savez_compressed(path, **d)
 
     @staticmethod
@@ -182,4 +203,7 @@ class ShudModel:
             setattr(m, k, z[k])
         if "ilake" in z.files:
             m.ilake = z["ilake"]
+        if "lake_bathy_off" in z.files:
+            m.lake_bathy_off, m.lake_bathy_y, m.lake_bathy_a = z["lake_bathy_off"], z["lake_bathy_y"], z["lake_bathy_a"]
+            m.num_lake = int(m.lake_bathy_off.size - 1)
         return m.finalize()

@@ -50,18 +50,20 @@ class RhsHandle:
             _check(lib().shud_rhs_create(C.byref(self._mesh), C.byref(self._par), C.byref(opt), C.byref(h)),
                    "shud_rhs_create")
             self.n_own, self.n_own_riv = model.num_ele, model.num_riv
+            self.n_lake = getattr(model, "num_lake", 0)
         else:
             self._part = partition.struct()
             _check(lib().shud_rhs_create_partitioned(C.byref(self._mesh), C.byref(self._par), C.byref(opt),
                                                      C.byref(self._part), C.byref(h)),
                    "shud_rhs_create_partitioned")
             self.n_own, self.n_own_riv = partition.n_own_ele, partition.n_own_riv
+            self.n_lake = 0                             # lakes: unpartitioned handles only
         self.h = h
         self.mode = mode
 
     @property
     def num_y(self):
-        return 3 * self.n_own + self.n_own_riv
+        return 3 * self.n_own + self.n_own_riv + self.n_lake
 
     def close(self):
         if self.h:
@@ -122,7 +124,8 @@ class RhsHandle:
         out = {}
         o = abi.ShudFluxOut()
         for name in abi.FLUXOUT_ORDER:
-            n = 3 * NE if name in abi.DIAG_ELE3 else NS if name in abi.DIAG_SEG else NR if name in abi.DIAG_RIV else NE
+            n = (3 * NE if name in abi.DIAG_ELE3 else NS if name in abi.DIAG_SEG else NR if name in abi.DIAG_RIV
+                 else getattr(m, "num_lake", 0) if name in abi.DIAG_LAKE else NE)
             out[name] = np.zeros(n)
             setattr(o, name, out[name].ctypes.data_as(abi.c_double_p))
         _check(lib().shud_rhs_sync_diagnostics(self.h, C.byref(o)), "shud_rhs_sync_diagnostics")

@@ -7,8 +7,9 @@ parsed with strtold then stored as double), Model_Data::read_mesh/att/soil/geol/
 Init:  Model_Data::initialize (src/ModelData/MD_initialize.cpp:168-245) via geometry.py, calibration
 (ModelConfigure.cpp:79-139, River.cpp:36-45), LoadIC mode 3 (MD_initialize.cpp:66-108).
 
-Lakes are out of scope: a project with lake elements loads but is flagged in
-model.ilake and rejected by shud_rhs_create.
+Lakes: lake ids from the .sp.att LAKE column, bathymetry tables from .lake.bathy
+(Model_Data::lake_readBathy, MD_Lake.cpp:147-168: one TabularData block per lake, columns INDEX, yi, ai),
+lake stages from the third .cfg.ic table (MD_initialize.cpp:86-99; 2.0 when the row count mismatches).
 """
 import os
 
@@ -208,6 +209,21 @@ def load_project(indir, prj, end_override=None):
     m.seg_riv = seg_riv.astype(np.int32)
     m.seg_length = rivseg[:, 3].copy()
     m.seg_cwr = R["Cwr"][rt[seg_riv]]                              # MD_initialize.cpp:220-226
+    # lakes: lakeon when any iLake > 0 (MD_readin.cpp:262-263); NumLake = LakeUniqueID (MD_Lake.cpp:12-29)
+    if np.any(m.ilake > 0):
+        NL = int(np.unique(m.ilake[m.ilake > 0]).size)
+        with open(p("lake.bathy")) as f:
+            bl = f.read().splitlines()
+        off, ys, as_, nxt = [0], [], [], 0
+        for _ in range(NL):
+            tb, nxt = read_table(bl, nxt)
+            ys.append(tb[:, 1])
+            as_.append(tb[:, 2])
+            off.append(off[-1] + tb.shape[0])
+        m.num_lake = NL
+        m.lake_bathy_off = np.array(off, dtype=np.int32)
+        m.lake_bathy_y = np.concatenate(ys)
+        m.lake_bathy_a = np.concatenate(as_)
     m.finalize()
     # IC (INIT_MODE 3): .cfg.ic element table [idx, canopy, snow, surf, unsat, gw], then river stage
     y0 = None
@@ -215,7 +231,11 @@ def load_project(indir, prj, end_override=None):
         with open(p("cfg.ic")) as f:
             il = f.read().splitlines()
         ice, nxt = read_table(il, 0)
-        icr, _ = read_table(il, nxt)
-        y0 = np.concatenate([ice[:NE, 3], ice[:NE, 4], ice[:NE, 5], icr[:NR, 1]])
+        icr, nxt = read_table(il, nxt)
+        parts = [ice[:NE, 3], ice[:NE, 4], ice[:NE, 5], icr[:NR, 1]]
+        if m.num_lake:
+            icl, _ = read_table(il, nxt)
+            parts.append(icl[:, 1] if icl.shape[0] == m.num_lake else np.full(m.num_lake, 2.))
+        y0 = np.concatenate(parts)
     m.meta.update(prj=prj, x=ext["x"], y=ext["y"], raised=ext["raised"], close_boundary=close_boundary)
     return m, {"y0": y0, "S": S, "G": G, "L": L, "R": R, "calib": g, "att": att}

@@ -16,7 +16,8 @@ def random_state(model, seed=12345, n_own=None, n_own_riv=None):
     us = rng.uniform(0.0, 1.0, NE) * 0.5 * aq
     gw = rng.uniform(0.0, 1.0, NE) * aq
     rv = rng.uniform(0.0, 2.0, NR)
-    return np.concatenate([sf, us, gw, rv])
+    lk = rng.uniform(0.0, 30.0, getattr(model, "num_lake", 0))     # lake stages (after the reaches)
+    return np.concatenate([sf, us, gw, rv, lk])
 
 
 def random_step_inputs(model, seed=777):
@@ -29,6 +30,8 @@ def random_step_inputs(model, seed=777):
     lai = np.where(rng.random(NE) < 0.2, 0.0, rng.uniform(0.0, 4.0, NE))
     e_ic = rng.uniform(0.0, 1.0, NE) * pot_tran * 1.2
     etp = pot_evap + pot_tran + rng.uniform(0.0, 1.0, NE) * day
+    u_satn = rng.uniform(0.0, 1.0, NE)
+    prcp = net_prep + rng.uniform(0.0, 5.0, NE) * day             # qElePrep (lake elements read it)
     return dict(net_prep=net_prep, pot_evap=pot_evap, pot_tran=pot_tran, etp=etp, lai=lai,
-                fu_surf=np.ones(NE), fu_sub=np.ones(NE), e_ic=e_ic, u_satn=rng.uniform(0.0, 1.0, NE),
-                ugw_stale=np.zeros(NE))
+                fu_surf=np.ones(NE), fu_sub=np.ones(NE), e_ic=e_ic, u_satn=u_satn,
+                ugw_stale=np.zeros(NE), prcp=prcp)

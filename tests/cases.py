@@ -19,6 +19,29 @@ def heihe():
     return m, y0
 
 
+def qhh():
+    """qhh: 4773 elements, 688 of them in one lake (.lake.bathy), bank edges around it."""
+    m, y0 = load_fixture("qhh")
+    m.step = workload.random_step_inputs(m, seed=13)
+    return m, y0
+
+
+def qhh_variant(seed=7):
+    """qhh with a few outlet reaches redirected into the lake (down = -4: toLake 0, MD_Lake.cpp:46-50),
+    fu != 1 and a low lake stage (exercises the 0.02 m dry guards and the qLakeEvap clamp)."""
+    m, y0 = load_fixture("qhh")
+    rng = np.random.default_rng(seed)
+    outs = np.nonzero(m.riv_down < 0)[0]
+    m.riv_down[outs[::3]] = -4
+    m.step = workload.random_step_inputs(m, seed=seed)
+    m.step["fu_surf"] = rng.uniform(0.5, 1.0, m.num_ele)
+    m.step["fu_sub"] = rng.uniform(0.5, 1.0, m.num_ele)
+    m.finalize()
+    y = workload.random_state(m, seed=seed + 1)
+    y[-1] = 0.01
+    return m, y
+
+
 def variant(n=2000, seed=5):
     """Synthetic mesh with CLOSEBOUNDARY 0, bank slopes, +-BC elements/reaches, SS flags, outlets."""
     m = synth.synth_model(n, seed=seed)

@@ -4,8 +4,9 @@ where /root/reference exists; the GPU box only reads the outputs).
 Writes:
   shud-up_amd/shud_rhs/data/ccw_tables.npz  ccw soil/geol/lc/river-type tables, calibration and the
                                             (iSoil, iGeol, iLC) rows of ccw.sp.att (synthetic meshes)
-  tests/golden/ccw_model.npz, heihe_model.npz  derived SoA after Model_Data::initialize() restated by
-                                            shud_rhs.shudio (inputs of the parity tests) + .cfg.ic state
+  tests/golden/ccw_model.npz, heihe_model.npz, qhh_model.npz  derived SoA after Model_Data::initialize()
+                                            restated by shud_rhs.shudio (inputs of the parity tests) + .cfg.ic
+                                            state (qhh: 688 lake elements, one lake, .lake.bathy table)
 These are input DATA (the reference ships no outputs / golden vectors for the RHS: SURVEY §4).
 """
 import os
@@ -19,6 +20,15 @@ sys.path.insert(0, os.path.join(ROOT, "shud-up_amd"))
 from shud_rhs import shudio  # noqa: E402
 
 REF = "/root/reference/input"
+
+
+def projects(names):
+    for prj in names:
+        m, ex = shudio.load_project(os.path.join(REF, prj), prj)
+        m.step = {}
+        m.save(os.path.join(HERE, f"{prj}_model.npz"))
+        np.save(os.path.join(HERE, f"{prj}_y0.npy"), ex["y0"])
+        print(prj, m.num_ele, m.num_riv, m.num_seg, m.num_lake, "sinks raised:", len(m.meta["raised"]))
 
 
 def main():
@@ -37,13 +47,11 @@ def main():
     np.savez_compressed(os.path.join(ROOT, "shud-up_amd", "shud_rhs", "data", "ccw_tables.npz"),
                         soil=soil, geol=geol, lc=lc, rtype=rtype, att_rows=att[:, 1:4].astype(np.int64),
                         calib_keys=np.array(keys), calib_vals=np.array([cal[k] for k in keys]))
-    for prj in ["ccw", "heihe"]:
-        m, ex = shudio.load_project(os.path.join(REF, prj), prj)
-        m.step = {}
-        m.save(os.path.join(HERE, f"{prj}_model.npz"))
-        np.save(os.path.join(HERE, f"{prj}_y0.npy"), ex["y0"])
-        print(prj, m.num_ele, m.num_riv, m.num_seg, "sinks raised:", len(m.meta["raised"]))
+    projects(["ccw", "heihe", "qhh"])
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1:
+        projects(sys.argv[1:])
+    else:
+        main()

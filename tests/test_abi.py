@@ -37,7 +37,7 @@ def test_library_exports_every_symbol():
     for n in header_functions():
         assert hasattr(lib, n), n
     abi.bind(lib)
-    assert lib.shud_rhs_abi_version() == 1
+    assert lib.shud_rhs_abi_version() == 2
 
 
 def _c_sizeof(struct):

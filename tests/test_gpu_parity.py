@@ -157,13 +157,35 @@ def test_error_paths(kind, oracle_mod, layout):
         assert fi[0] == idx
 
 
-def test_lake_rejected():
+def test_lake_without_bathymetry_rejected():
     rt = _runtime()
     m, _ = cases.ccw()
     m.ilake = np.zeros(m.num_ele, dtype=np.int32)
-    m.ilake[5] = 1
+    m.ilake[5] = 1                                   # a lake element but num_lake = 0
     with pytest.raises(rt.ShudRhsError) as ei:
         rt.RhsHandle(m)
+    assert ei.value.code == abi.SHUD_ERR_ARG
+
+
+@pytest.mark.parametrize("case", ["qhh", "qhh_variant"])
+def test_lakes(case, oracle_mod):
+    """Lake module (SURVEY §8f f3): qhh (688 lake elements, bank edges) and reaches redirected into the lake;
+    IC state, a low and a high lake stage, 3 stateful calls each, every diagnostic incl. the lake sums."""
+    m, y = getattr(cases, case)()
+    ys = [y.copy(), workload.random_state(m, seed=31)]
+    ys[1][-1] = 300.0                                 # lake level above its banks: weir exchange both ways
+    _compare_sequence(m, ys, abi.SHUD_MODE_SERIAL, oracle_mod, label=case, layout="packed")
+
+
+def test_lakes_unsupported_modes(monkeypatch):
+    rt = _runtime()
+    m, _ = cases.qhh()
+    with pytest.raises(rt.ShudRhsError) as ei:
+        rt.RhsHandle(m, mode=abi.SHUD_MODE_OMP)       # the OMP path has no lake physics
+    assert ei.value.code == abi.SHUD_ERR_UNSUPPORTED
+    monkeypatch.setenv("SHUD_RHS_PACKED", "0")
+    with pytest.raises(rt.ShudRhsError) as ei:
+        rt.RhsHandle(m)                               # lakes need the packed layout
     assert ei.value.code == abi.SHUD_ERR_UNSUPPORTED
 
 
