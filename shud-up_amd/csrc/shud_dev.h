@@ -124,6 +124,11 @@ struct YView {
     __device__ __forceinline__ double us(int i) const { return i < n_own ? y[n_own + i] : gele[3 * (i - n_own) + 1]; }
     __device__ __forceinline__ double gw(int i) const { return i < n_own ? y[2 * n_own + i] : gele[3 * (i - n_own) + 2]; }
     __device__ __forceinline__ double riv(int r) const { return r < n_own_riv ? y[3 * n_own + r] : griv[r - n_own_riv]; }
+    // GH = false: an unpartitioned handle has no ghosts, every index is owned (no select per access)
+    template <bool GH> __device__ __forceinline__ double sf_(int i) const { return GH ? sf(i) : y[i]; }
+    template <bool GH> __device__ __forceinline__ double us_(int i) const { return GH ? us(i) : y[n_own + i]; }
+    template <bool GH> __device__ __forceinline__ double gw_(int i) const { return GH ? gw(i) : y[2 * n_own + i]; }
+    template <bool GH> __device__ __forceinline__ double riv_(int r) const { return GH ? riv(r) : y[3 * n_own + r]; }
 #endif
 };
 

@@ -42,6 +42,15 @@ __device__ __forceinline__ void stnt2(double2 *p, double a, double b) {
     __builtin_nontemporal_store(v, (v2d *)p);
 }
 
+#ifndef SHUD_AREA_EARLY
+#define SHUD_AREA_EARLY 1
+#endif
+// IEEE class tests (one v_cmp_class_f64 each): NaN | +-inf, and NaN | +-inf | negative (not -0.0)
+__device__ __forceinline__ bool nan_or_inf(double x) { return __builtin_isfpclass(x, 0x0003 | 0x0004 | 0x0200); }
+__device__ __forceinline__ bool bad_nonneg(double x) {
+    return __builtin_isfpclass(x, 0x0003 | 0x0004 | 0x0008 | 0x0010 | 0x0200);
+}
+
 // packed cf word (DevPacked::meta.w)
 __device__ __forceinline__ int cf_ibc(int cf) { return (int)(int8_t)(cf & 0xff); }
 __device__ __forceinline__ int cf_iss(int cf) { return (cf >> 8) & 3; }
@@ -70,7 +79,7 @@ constexpr int CF_LDS_STRIDE = CF_COUNT | 1;
 // fun_Ele_lakeVertical / fun_Ele_lakeHorizon (Element.cpp:336-346, MD_ElementFlux.cpp:2-23) and get zero DY
 // (MD_f.cpp:146-150); bank edges of other elements exchange with the lake (MD_ElementFlux.cpp:46-53,107-121)
 // and leave their fluxes in DevLake for the lake kernel.  LAKE = false compiles all of it away.
-template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE>
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
 __global__ void __launch_bounds__(256, 5)
 shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int i0, int n_compute, int cur,
                        DevDiag dg, DevLake lk) {
@@ -92,7 +101,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     // while little else is live ----------------
     const int4 mt = p.meta[i];
     const double2 zz = p.zz[i];
-    const double ysf_raw = Y.sf(i), yus_raw = Y.us(i), ygw_raw = Y.gw(i);
+    const double ysf_raw = Y.sf_<GH>(i), yus_raw = Y.us_<GH>(i), ygw_raw = Y.gw_<GH>(i);
     const int cf = mt.w;
     const int cid = cf_class(cf), ibc = cf_ibc(cf);
     const bool is_lake = LAKE && cf < 0;
@@ -158,15 +167,12 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         } else { Tg = Tu = eic = 0.; }
         const double trans = Tg + Tu, evapo = Eu + Eg + Es, eta = eic + evapo + trans;
         report_w(m.err, eta > etp * 2., 0x10u, 4, i, true);      // printf warning, MD_ET.cpp:391-393
-        bool neg = false;                                         // CheckNonNegative, functions.cpp:148-154
-        neg |= (Es < 0.0 || isnan(Es) || isinf(Es) || fabs(Es - K_NA_VALUE) < K_ZERO);
-        neg |= (Eu < 0.0 || isnan(Eu) || isinf(Eu) || fabs(Eu - K_NA_VALUE) < K_ZERO);
-        neg |= (Eg < 0.0 || isnan(Eg) || isinf(Eg) || fabs(Eg - K_NA_VALUE) < K_ZERO);
-        neg |= (Tu < 0.0 || isnan(Tu) || isinf(Tu) || fabs(Tu - K_NA_VALUE) < K_ZERO);
-        neg |= (Tg < 0.0 || isnan(Tg) || isinf(Tg) || fabs(Tg - K_NA_VALUE) < K_ZERO);
+        // CheckNonNegative (functions.cpp:148-154): x < 0 || isnan || isinf || |x - NA| < ZERO is exactly
+        // "NaN, an infinity, or a negative normal/subnormal" (-0.0 passes; x ~ -9999 is negative): one
+        // v_cmp_class per value
+        const bool neg = bad_nonneg(Es) || bad_nonneg(Eu) || bad_nonneg(Eg) || bad_nonneg(Tu) || bad_nonneg(Tg);
         report_w(m.err, neg, 0x04u, 2, i);
-        report_w(m.err, !neg && (isnan(eta) || isinf(eta) || isnan(evapo) || isinf(evapo) || isnan(trans) ||
-                                 isinf(trans)), 0x08u, 3, i);
+        report_w(m.err, !neg && (nan_or_inf(eta) || nan_or_inf(evapo) || nan_or_inf(trans)), 0x08u, 3, i);
         if (DIAG) { dg.q_es[i] = Es; dg.q_eu[i] = Eu; dg.q_eg[i] = Eg; dg.q_tu[i] = Tu; dg.q_tg[i] = Tg;
                     dg.q_eta[i] = eta; dg.i_beta[i] = ibeta; }
     }
@@ -220,7 +226,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
             const double2 lc = p.sg_lc[k], dk = p.sg_dk[k];
             const int2 rb = p.sg_rb[k];
             const double bt = p.sg_bt[k];
-            double yr = Y.riv(rb.x);                      // uriv_of (shud_physics.h), BC from the record
+            double yr = Y.riv_<GH>(rb.x);                 // uriv_of (shud_physics.h), BC from the record
             if (MODE == 1) yr = (yr >= 0.) ? yr : 0.;
             if (rb.y > 0) yr = m.rybc[rb.y];
             const double rdep = dk.x, L = lc.x;
@@ -244,6 +250,9 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     double sumsurf = qe2r_surf, sumsub = qe2r_sub;     // QeleSurfTot = Qe2r + sum_j QeleSurf[j]
     bool nan_q = false;
     const double isf = usf < 0. ? 0. : usf;
+#if SHUD_AREA_EARLY
+    const double area = ldnt(&p.area[i]);              // in flight across the edge loop
+#endif
 #pragma unroll 1
     for (int j = 0; j < (is_lake ? 0 : 3); j++) {     // lake elements: fun_Ele_lakeHorizon, all zero
         const int nb = j == 0 ? mt.x : j == 1 ? mt.y : mt.z;
@@ -251,7 +260,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         const int nc = nb >= 0 ? nb : i;                  // boundary edge: harmless in-bounds loads
         const double2 nzz = p.zz[nc];
         const int ncf = p.meta[nc].w;
-        const double nsf_raw = Y.sf(nc), ngw_raw = Y.gw(nc);
+        const double nsf_raw = Y.sf_<GH>(nc), ngw_raw = Y.gw_<GH>(nc);
         const double B = g.x, d2n = g.y;
         double qsf = 0., qsb = 0.;
         const int cn = cf_class(ncf);
@@ -319,7 +328,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
             qsb = q * fu_sub;
         }
 #undef CN
-        if (MODE == 0) nan_q |= (isnan(qsf) || isinf(qsf) || isnan(qsb) || isinf(qsb));
+        if (MODE == 0) nan_q |= nan_or_inf(qsf) || nan_or_inf(qsb);
         sumsurf += qsf;
         sumsub += qsb;
         if (DIAG) { dg.qele_surf[j * NEl + i] = qsf; dg.qele_sub[j * NEl + i] = qsb; }
@@ -329,7 +338,9 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     if (MODE == 0) report_w(m.err, nan_q, 0x01u, 0, i);       // CheckNANij, MD_f.cpp:73-74
 
     // ---- f_applyDY element part (MD_f.cpp:88-150 / MD_f_omp.cpp:26-46) ----
+#if !SHUD_AREA_EARLY
     const double area = ldnt(&p.area[i]);
+#endif
     double dsf = dsf_head - SDIV(sumsurf, area) - Es;
     double dgw = dgw_head - SDIV(sumsub, area) - Eg - Tg;
     if (ibc > 0) dgw = 0;
@@ -569,13 +580,13 @@ shud_pack_step_kernel(DevMesh m, DevPacked p, int n, int cur, unsigned what) {
     if (what & 16) p.cs[cur][i].y = m.e_ic[0][i];
 }
 
-template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE>
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
 static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1, int cur,
                      const DevDiag &dg, const DevLake &lk, hipStream_t s) {
     int nb = (i1 - i0 + 255) / 256;
     nb = (nb + 7) / 8 * 8;                  // block_id<1> deals blocks to XCDs in contiguous chunks
     const size_t lds = LCT ? (size_t)p.ncls * CF_LDS_STRIDE * sizeof(double) : 0;
-    hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT, LAKE>), dim3(nb), dim3(256), lds, s, m, p,
+    hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH>), dim3(nb), dim3(256), lds, s, m, p,
                        Y, dy, i0, i1, cur, dg, lk);
 }
 
@@ -586,10 +597,13 @@ void launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YV
     DevLake lk{};
     if (lake) lk = *lake;
     // lakes: serial semantics only (the handle rejects OMP + lakes), class table in LDS
+    const bool gh = Y.gele != nullptr || Y.griv != nullptr;      // partitioned handle: ghost entities
 #define LP(MO, OP, DI, FU) do {                                                                            \
-        if (lake && MO == 0) launch_p<MO, OP, DI, FU, true, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s);    \
-        else if (p.ncls <= LDS_CLS_MAX) launch_p<MO, OP, DI, FU, true, false>(m, p, Y, dy, i0, i1, cur, dg, lk, s); \
-        else launch_p<MO, OP, DI, FU, false, false>(m, p, Y, dy, i0, i1, cur, dg, lk, s); } while (0)
+        if (lake && MO == 0) launch_p<MO, OP, DI, FU, true, true, false>(m, p, Y, dy, i0, i1, cur, dg, lk, s); \
+        else if (p.ncls <= LDS_CLS_MAX) {                                                                 \
+            if (gh) launch_p<MO, OP, DI, FU, true, false, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s);     \
+            else launch_p<MO, OP, DI, FU, true, false, false>(m, p, Y, dy, i0, i1, cur, dg, lk, s);       \
+        } else launch_p<MO, OP, DI, FU, false, false, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s); } while (0)
 #define LFU(MO, OP, DI) do { if (fu_unit) LP(MO, OP, DI, true); else LP(MO, OP, DI, false); } while (0)
 #define LDI(MO, OP) do { if (diag) LFU(MO, OP, true); else LFU(MO, OP, false); } while (0)
 #define LOP(MO) do { if (open) LDI(MO, true); else LDI(MO, false); } while (0)

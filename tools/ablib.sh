@@ -7,4 +7,5 @@ name=$1; shift
 mkdir -p build/ab/$name
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -I../include -Icsrc"
 /opt/rocm/bin/hipcc $F "$@" -c csrc/shud_ele_packed.hip -o build/ab/$name/p.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o build/ab/libshud_rhs_$name.so build/shud_kernels.o build/ab/$name/p.o build/shud_rhs.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+others=$(ls build/*.o | grep -v shud_ele_packed.o)
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o build/ab/libshud_rhs_$name.so build/ab/$name/p.o $others -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
