@@ -76,7 +76,9 @@ struct DevPacked {
     const double2 *sg_dk;   //   its reach's {depth, KsatH}
     const int2 *sg_rb;      //   {reach, reach BC column}
     const double *sg_bt;    //   its reach's BedThick
-    double2 *qseg2;         // [NS] element-sorted {QsegSurf, QsegSub}, written by the element kernel
+    double2 *qseg2;         // [NS] {QsegSurf, QsegSub}, written by the element kernel (element-sorted, or
+                            //   reach-sorted when seg_rpos is set)
+    const int *seg_rpos;    // nullptr, or element-sorted k -> reach-sorted slot (SHUD_RHS_SEG_ORDER=reach)
     double2 *s_np;          // {net_prep, pot_evap}        step inputs (packed by shud_pack_step_kernel)
     double2 *s_tl;          // {pot_tran, lai}
     double2 *s_fu;          // {fu_surf, fu_sub}            read only when not all ones

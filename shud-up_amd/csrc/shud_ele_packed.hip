@@ -232,7 +232,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
             const double rdep = dk.x, L = lc.x;
             const double qs = weir_jtoi(zs, isf_seg, zs - rdep, yr, zs + 0.0, lc.y, L, dep);
             const double qg = r2e_gw(yr, zs - rdep, ugw, zb, ekh, dk.y, L, bt) * fu_sub;
-            p.qseg2[k] = make_double2(qs, qg);    // element-sorted: consecutive lanes, consecutive k
+            p.qseg2[p.seg_rpos ? p.seg_rpos[k] : k] = make_double2(qs, qg);   // element-sorted by default
             qe2r_surf += -qs;
             qe2r_sub += -qg;
         }
@@ -445,6 +445,13 @@ shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     // fluxes (scattered 8-B writes from the element kernel cost more than these gathers).  Batches of 8:
     // all index loads, then all gathers, are in flight together; the adds stay in segment order
     double qsurf = 0., qsub = 0.;
+    if (p.seg_rpos) {                            // reach-sorted fluxes: this reach's segments are contiguous
+        for (int k = ii.z, k1 = ii.z + ii.w; k < k1; k++) {
+            const double2 q2 = p.qseg2[k];
+            qsurf += q2.x;
+            qsub += q2.y;
+        }
+    } else
     for (int k0 = ii.z, k1 = ii.z + ii.w; k0 < k1; k0 += 8) {
         int ps[8];
 #pragma unroll

@@ -66,6 +66,7 @@ struct shud_rhs {
     int last_cur = 0, last_cur_e = 0;
 
     std::vector<int> seg_perm;           // element-sorted position -> reference segment index
+    std::vector<int> rseg_perm;          // reach-sorted position -> reference segment index (SEG_ORDER=reach)
     int max_col[4] = {0, 0, 0, 0};       // highest BC column referenced: eyBC, eqBC, ryBC, rqBC
     double *d_tab[4] = {nullptr, nullptr, nullptr, nullptr};
     int tab_len[4] = {0, 0, 0, 0};

@@ -435,6 +435,17 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     std::vector<int> rstart(NR, 0), rcnt(NR, 0);
     for (int q = NS - 1; q >= 0; q--) rstart[m->seg_riv[rorder[q]]] = q;
     for (int s = 0; s < NS; s++) rcnt[m->seg_riv[s]]++;
+    // SHUD_RHS_SEG_ORDER=reach (A/B): the element kernel scatters each segment's flux pair to its reach-sorted
+    // slot and the river kernel reads its segments contiguously; default: element order + gathers
+    if (const char *so = getenv("SHUD_RHS_SEG_ORDER"); so && !strcmp(so, "reach") && !h->partitioned) {
+        std::vector<int> rpos_of(NS), rpos(NS);
+        for (int q = 0; q < NS; q++) rpos_of[rorder[q]] = q;
+        for (int k = 0; k < NS; k++) rpos[k] = rpos_of[h->seg_perm[k]];
+        int *rp_d;
+        if ((rc = h->upload(&rp_d, rpos.data(), NS))) return rc;
+        P.seg_rpos = rp_d;
+        h->rseg_perm = rorder;
+    }
     std::vector<double2> ra(NR), rb(NR), rcc(NR), rd(NR);
     std::vector<int4> ri(NR), ru(NR);
     const int nor = h->n_own_riv;
@@ -913,7 +924,7 @@ extern "C" int shud_rhs_sync_diagnostics(shud_rhs_t h, ShudFluxOut *o) {
     std::vector<double> tmp;
     if (o->qseg_surf || o->qseg_sub) tmp.resize(std::max<size_t>(NS, 1));
     HIP_TRY(hipStreamSynchronize(h->stream));
-    const std::vector<int> &perm = h->seg_perm;
+    const std::vector<int> &perm = (h->packed && h->dp.seg_rpos) ? h->rseg_perm : h->seg_perm;
     if (h->packed && !h->variant && NS && (o->qseg_surf || o->qseg_sub)) {
         std::vector<double2> q2(NS);
         HIP_TRY(hipMemcpy(q2.data(), h->dp.qseg2, NS * sizeof(double2), hipMemcpyDeviceToHost));

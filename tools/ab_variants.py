@@ -29,7 +29,8 @@ vs = a.variants.split(",")
 def env_for(v):
     if v.startswith("soa"):
         return {"SHUD_RHS_PACKED": "0", "SHUD_RHS_ELE_VARIANT": v[3:] or "0"}
-    return {"SHUD_RHS_PACKED": "1", "SHUD_RHS_ELE_VARIANT": "0"}
+    return {"SHUD_RHS_PACKED": "1", "SHUD_RHS_ELE_VARIANT": "0",
+            "SHUD_RHS_SEG_ORDER": "reach" if v == "pkR" else "element"}
 res = {v: [] for v in vs}
 ref = None
 for rnd in range(a.rounds):
