@@ -149,3 +149,80 @@ class OracleEt:
                 self.h = None
         except Exception:  # noqa: BLE001
             pass
+
+
+class OracleOde:
+    """CPU restatement of the CVODE 6.0.0 BDF/Newton/SPGMR integrator (shud_oracle_ode.c).
+
+    rhs: an OracleRhs (the SHUD RHS) or a built-in test problem "robertson" / "decay" / "decayn"."""
+
+    STATS = ["nst", "nfe", "nfe_ls", "nni", "ncfn", "nnf", "netf", "nsetups", "nli", "ncfl", "njtimes", "qlast",
+             "qcur"]
+    RSTATS = ["hlast", "hcur", "tcur", "hnext"]
+
+    def __init__(self, rhs, t0, y0, rtol, atol, init_step, max_step=0.0, min_step=1e-6, max_num_steps=1000000,
+                 maxl=0):
+        L = lib()
+        if not getattr(L, "_ode_bound", False):
+            vp, d, lg = C.c_void_p, C.c_double, C.c_long
+            L.oracle_ode_create_shud.restype = vp
+            L.oracle_ode_create_shud.argtypes = [vp, lg, d, vp, d, d, d, d, d, lg, C.c_int]
+            L.oracle_ode_create_test.restype = vp
+            L.oracle_ode_create_test.argtypes = [C.c_int, lg, d, vp, d, d, d, d, d, lg, C.c_int]
+            L.oracle_ode_solve.restype = C.c_int
+            L.oracle_ode_solve.argtypes = [vp, d, vp, C.POINTER(d), C.c_int]
+            L.oracle_ode_get_dky.restype = C.c_int
+            L.oracle_ode_get_dky.argtypes = [vp, d, C.c_int, vp]
+            L.oracle_ode_set_stop_time.argtypes = [vp, d]
+            L.oracle_ode_get_stats.argtypes = [vp, vp, vp]
+            L.oracle_ode_destroy.argtypes = [vp]
+            L.oracle_ode_set_reduction_order.argtypes = [C.c_int]
+            L._ode_bound = True
+        self._y0 = np.ascontiguousarray(y0, dtype=np.float64).copy()
+        self.n = self._y0.size
+        args = (float(t0), self._y0.ctypes.data, float(rtol), float(atol), float(init_step), float(max_step),
+                float(min_step), int(max_num_steps), int(maxl))
+        if isinstance(rhs, str):
+            prob = {"robertson": 1, "decay": 2, "decayn": 3}[rhs]
+            self.h = L.oracle_ode_create_test(prob, self.n, *args)
+        else:
+            self._rhs = rhs                                   # keep the OracleRhs alive
+            self.h = L.oracle_ode_create_shud(rhs.h, self.n, *args)
+        if not self.h:
+            raise ValueError("oracle_ode_create: invalid options")
+
+    @staticmethod
+    def set_reduction_order(order):
+        """0: serial N_Vector order (CVODE's); 1: the device integrator's fixed blocked order"""
+        lib().oracle_ode_set_reduction_order(int(order))
+
+    def set_stop_time(self, tstop):
+        lib().oracle_ode_set_stop_time(self.h, float(tstop))
+
+    def solve(self, tout, one_step=False):
+        """CVode(mem, tout, y, &t, CV_NORMAL | CV_ONE_STEP) -> (flag, t, y)"""
+        y = np.empty(self.n)
+        t = C.c_double()
+        flag = lib().oracle_ode_solve(self.h, float(tout), y.ctypes.data, C.byref(t), 2 if one_step else 1)
+        return flag, t.value, y
+
+    def get_dky(self, t, k):
+        d = np.empty(self.n)
+        flag = lib().oracle_ode_get_dky(self.h, float(t), int(k), d.ctypes.data)
+        return flag, d
+
+    def stats(self):
+        c = (C.c_long * 16)()
+        r = (C.c_double * 8)()
+        lib().oracle_ode_get_stats(self.h, c, r)
+        out = {k: c[i] for i, k in enumerate(self.STATS)}
+        out.update({k: r[i] for i, k in enumerate(self.RSTATS)})
+        return out
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().oracle_ode_destroy(self.h)
+                self.h = None
+        except Exception:  # noqa: BLE001
+            pass

@@ -59,3 +59,52 @@ extern "C" int shud_kat_eval(int fn, const double *h_in, int n, double *h_out) {
     (void)hipFree(d_out);
     return rc;
 }
+
+// ---- published ODE test problems on the device, for the integrator (tests/test_gpu_ode.py) ----
+// Same expressions, same order as oracle/shud_oracle_ode.c (robertson_rhs, decay_rhs, decayn_rhs).
+struct KatOde {
+    int problem;
+    hipStream_t s;
+};
+__constant__ double kat_decay_lam[3] = {1.0, 10.0, 1000.0};
+__constant__ double kat_decayn_lam[7] = {0.01, 0.1, 1.0, 10.0, 100.0, 1000.0, 10000.0};
+
+__global__ void kat_ode_kernel(int problem, int64_t n, const double *__restrict__ y, double *__restrict__ yd) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (problem == 1) {                                          // Robertson (1966)
+        if (i != 0) return;
+        const double y1 = y[0], y2 = y[1], y3 = y[2];
+        const double a = -0.04 * y1 + 1.0e4 * y2 * y3;
+        const double c = 3.0e7 * y2 * y2;
+        yd[0] = a;
+        yd[2] = c;
+        yd[1] = -a - c;
+    } else if (problem == 2) {
+        if (i < 3) yd[i] = -kat_decay_lam[i] * y[i];
+    } else if (i < n) {
+        yd[i] = -kat_decayn_lam[i % 7] * y[i];
+    }
+}
+
+extern "C" void *shud_kat_ode_user(int problem) {
+    KatOde *u = new KatOde{problem, nullptr};
+    if (hipStreamCreate(&u->s) != hipSuccess) { delete u; return nullptr; }
+    return u;
+}
+extern "C" void *shud_kat_ode_stream(void *u) { return u ? ((KatOde *)u)->s : nullptr; }
+static int64_t kat_ode_n = 0;
+extern "C" void shud_kat_ode_set_n(int64_t n) { kat_ode_n = n; }
+extern "C" int shud_kat_ode_rhs(double t, const double *y, double *yd, void *user) {
+    (void)t;
+    KatOde *u = (KatOde *)user;
+    const int64_t n = u->problem == 3 ? kat_ode_n : 3;
+    hipLaunchKernelGGL(kat_ode_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, u->s, u->problem, n, y, yd);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+extern "C" void shud_kat_ode_free(void *user) {
+    KatOde *u = (KatOde *)user;
+    if (!u) return;
+    (void)hipStreamSynchronize(u->s);
+    (void)hipStreamDestroy(u->s);
+    delete u;
+}

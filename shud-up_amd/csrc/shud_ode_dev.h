@@ -1,0 +1,94 @@
+// shud_ode_dev.h — internal: device vector kernels of the integrator (shud_ode_kernels.hip), called by the
+// host controller (shud_ode.cpp).  Not part of the C-ABI.
+//
+// Every kernel is one streaming pass over NY-long fp64 vectors in HBM, fusing the N_Vector operations that
+// CVODE issues back to back (cvode.c / sunlinsol_spgmr.c / nvector_serial.c) so each pass reads every operand
+// once.  Per element the arithmetic is exactly the serial N_Vector kernel's (same operations, same order, no
+// FMA contraction: -ffp-contract=off).  Reductions (dot products, WRMS norms, min) are deterministic: a fixed
+// grid writes per-block partials in a fixed order, and a one-block finalize kernel sums them in a fixed order
+// into a device scalar slot `ds[slot]` that later kernels read directly (no host round trip) or the host fetches.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace shud {
+namespace ode {
+
+constexpr int kThreads = 256;
+constexpr int kMaxBlocks = 2048;
+constexpr int kMaxAcc = 4;
+constexpr int kMaxL = 32;     // SPGMR Krylov dimension bound (maxl)
+constexpr int kQMax = 5;      // BDF
+
+// device scalar slots
+enum Slot : int {
+    S_EWTMIN = 0,   // min(rtol|y| + atol)
+    S_NRM,          // sum (zn0*ewt)^2
+    S_RES,          // sum (delta*ewt)^2 of the Newton residual (bnorm and SPGMR beta)
+    S_SIG,          // sum ((V/ewt)*ewt)^2 of the current Krylov vector (DQ perturbation)
+    S_WN,           // sum w*w after Gram-Schmidt (new_vk_norm^2)
+    S_DEL,          // sum (delta*ewt)^2 of the Newton update
+    S_YCOR,         // sum (ycor*ewt)^2
+    S_ETAQM1,       // sum (zn[q]*ewt)^2
+    S_ETAQP1,       // sum (((-cquot) zn[qmax] + acor)*ewt)^2
+    S_W = 15,       // sum w*w before Gram-Schmidt (vk_norm^2); atimes writes [S_W, S_H0]
+    S_H0 = 16,      // S_H0 + i: Gram-Schmidt coefficient h[i][l] (first pass), i <= kMaxL
+    S_R0 = S_H0 + kMaxL + 1,   // S_R0 + i: reorthogonalisation products
+    S_COUNT = S_R0 + kMaxL + 1
+};
+
+struct Red {           // partial-sum scratch of one reduction launch
+    double *part;      // [kMaxAcc][kMaxBlocks]
+    int nblk;          // blocks of the producing grid (fixed per n)
+};
+
+struct Coefs {         // small host-computed coefficient arrays passed by value
+    double c[kMaxL + 1];
+};
+
+// ---- launchers (hipStream_t s) ----
+void finalize(const Red &r, int nacc, unsigned minmask, double *ds, int slot0, hipStream_t s);
+
+void ewt_set(int64_t n, const double *zn0, double *ewt, double rtol, double atol, const Red &r, hipStream_t s);
+void predict(int64_t n, double *zn, int q, hipStream_t s);
+void restore(int64_t n, double *zn, int q, hipStream_t s);
+void rescale(int64_t n, double *zn, int q, const Coefs &c, hipStream_t s);
+void vsum(int64_t n, const double *x, const double *y, double *z, hipStream_t s);
+void copy(int64_t n, const double *x, double *z, hipStream_t s);
+void scale_to(int64_t n, double c, const double *x, double *z, hipStream_t s);
+void zero(int64_t n, double *z, hipStream_t s);
+// zn[j] = coef[j] * zn[src] + zn[j], j in [jlo, jhi]
+void axpy_multi(int64_t n, double *zn, int src, const Coefs &coef, int jlo, int jhi, hipStream_t s);
+// Newton residual: delta = -((rl1*zn1 + ycor) + ngamma*ftemp); r: sum (delta*ewt)^2
+void residual(int64_t n, const double *zn1, const double *ycor, const double *ftemp, double rl1, double ngamma,
+              const double *ewt, double *delta, const Red &r, hipStream_t s);
+// V0 = c * (ewt*delta); r: sum ((V0/ewt)*ewt)^2
+void krylov_v0(int64_t n, const double *delta, const double *ewt, double c, double *V0, const Red &r, hipStream_t s);
+// work = sig*(V/ewt) + y, sig = 1/sqrt(ds[S_SIG]/n)
+void dq_work(int64_t n, const double *V, const double *ewt, const double *y, double *work, const double *ds,
+             hipStream_t s);
+// w (in: f(work)) = ewt * ((-gamma)*(siginv*(w - fy)) + V/ewt); r: [sum w*w, sum V0*w]
+void atimes(int64_t n, double *w, const double *fy, const double *V, const double *ewt, const double *V0,
+            double ngamma, const double *ds, const Red &r, hipStream_t s);
+// w = w + (-ds[hslot])*Vprev (if Vprev); r: sum Vnext*w (Vnext) or sum w*w
+void mgs(int64_t n, double *w, const double *Vprev, const double *ds, int hslot, const double *Vnext, const Red &r,
+         hipStream_t s);
+// w = c*w; r: sum ((w/ewt)*ewt)^2
+void normalize(int64_t n, double *w, double c, const double *ewt, const Red &r, hipStream_t s);
+// Newton update: delta = (sum_k yg[k] V_k)/ewt (krydim > 0), or delta = dsrc (krydim 0; NULL = 0);
+// ycor += delta; r: [sum (delta*ewt)^2, sum (ycor*ewt)^2]
+void newton_update(int64_t n, const double *V, int64_t vstride, int krydim, const Coefs &yg, const double *dsrc,
+                   const double *ewt, double *ycor, const Red &r, hipStream_t s);
+// zn[j] = l[j]*acor + zn[j], j = 0..q; if copy_to >= 0: zn[copy_to] = acor
+void complete_step(int64_t n, double *zn, const double *acor, const Coefs &l, int q, int copy_to, hipStream_t s);
+// r: [sum (zn_q*ewt)^2 (zn_q != NULL), sum (((-cquot)*zn_qmax + acor)*ewt)^2 (zn_qmax != NULL)]
+void eta_norms(int64_t n, const double *zn_q, const double *zn_qmax, const double *acor, double ncquot,
+               const double *ewt, const Red &r, hipStream_t s);
+// dky = lincomb(c, zn[js]) (N_VLinearCombination), then dky *= rscale if rscale != 0
+void dky(int64_t n, const double *zn, int64_t stride, const int *js, const Coefs &c, int nvec, double rscale,
+         double *out, hipStream_t s);
+int grid_blocks(int64_t n);
+
+}  // namespace ode
+}  // namespace shud

@@ -1,0 +1,392 @@
+// shud_ode_kernels.hip — device vector kernels of the integrator (see shud_ode_dev.h).
+//
+// Streaming passes over fp64 vectors of NY entries (grid-stride, 256-thread blocks, grid fixed per NY so every
+// reduction is deterministic).  Per element each kernel applies exactly the serial N_Vector operations CVODE
+// issues (nvector_serial.c: N_VLinearSum special cases, N_VScale, N_VProd/N_VDiv, N_VLinearCombination,
+// N_VScaleAddMulti) in the same order; the host controller (shud_ode.cpp) cites the CVODE routine each call
+// replaces.  The bound is HBM bandwidth: bytes per entry are listed at each kernel.
+#include "shud_ode_dev.h"
+
+#include <cmath>
+
+namespace shud {
+namespace ode {
+
+int grid_blocks(int64_t n) {
+    int64_t b = (n + kThreads - 1) / kThreads;
+    if (b < 1) b = 1;
+    return (int)(b < kMaxBlocks ? b : kMaxBlocks);
+}
+
+#define GRID_LOOP(i, n) for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < (n); i += (int64_t)gridDim.x * kThreads)
+
+__device__ inline double comb(double a, double b, bool mn) { return mn ? fmin(a, b) : a + b; }
+
+// block partials: wave64 butterfly, then the 4 wave results in wave order (deterministic)
+template <int NACC>
+__device__ inline void block_partial(double (&v)[NACC], unsigned minmask, const Red &r) {
+    __shared__ double sm[NACC][kThreads / 64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int a = 0; a < NACC; ++a) {
+        const bool mn = (minmask >> a) & 1u;
+        double x = v[a];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) x = comb(x, __shfl_xor(x, off, 64), mn);
+        if (lane == 0) sm[a][wid] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int a = 0; a < NACC; ++a) {
+            const bool mn = (minmask >> a) & 1u;
+            double s = sm[a][0];
+            for (int w = 1; w < kThreads / 64; ++w) s = comb(s, sm[a][w], mn);
+            r.part[(int64_t)a * kMaxBlocks + blockIdx.x] = s;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kThreads) k_finalize(const double *__restrict__ part, int nacc, int nblk,
+                                                       unsigned minmask, double *__restrict__ ds, int slot0) {
+    __shared__ double sm[kThreads / 64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int a = 0; a < nacc; ++a) {
+        const bool mn = (minmask >> a) & 1u;
+        double x = mn ? INFINITY : 0.0;
+        for (int b = threadIdx.x; b < nblk; b += kThreads) x = comb(x, part[(int64_t)a * kMaxBlocks + b], mn);
+        for (int off = 32; off >= 1; off >>= 1) x = comb(x, __shfl_xor(x, off, 64), mn);
+        if (lane == 0) sm[wid] = x;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double s = sm[0];
+            for (int w = 1; w < kThreads / 64; ++w) s = comb(s, sm[w], mn);
+            ds[slot0 + a] = s;
+        }
+        __syncthreads();
+    }
+}
+
+void finalize(const Red &r, int nacc, unsigned minmask, double *ds, int slot0, hipStream_t s) {
+    k_finalize<<<1, kThreads, 0, s>>>(r.part, nacc, r.nblk, minmask, ds, slot0);
+}
+
+// cvEwtSetSS + the N_VWrmsNorm(zn[0], ewt) of CVode's "too much accuracy" check.  24 B/entry.
+__global__ void __launch_bounds__(kThreads) k_ewt(int64_t n, const double *__restrict__ zn0, double *__restrict__ ewt,
+                                                  double rtol, double atol, Red r) {
+    double v[2] = {INFINITY, 0.0};
+    GRID_LOOP(i, n) {
+        const double y = zn0[i];
+        const double t = rtol * fabs(y) + atol;
+        const double w = 1.0 / t;
+        ewt[i] = w;
+        v[0] = fmin(v[0], t);
+        const double p = y * w;
+        v[1] += p * p;
+    }
+    block_partial<2>(v, 1u, r);
+}
+void ewt_set(int64_t n, const double *zn0, double *ewt, double rtol, double atol, const Red &r, hipStream_t s) {
+    k_ewt<<<r.nblk, kThreads, 0, s>>>(n, zn0, ewt, rtol, atol, r);
+}
+
+// cvPredict / cvRestore: Pascal-triangle update of the Nordsieck array in registers.  2*8*(q+1) B/entry.
+template <int Q, bool FWD>
+__global__ void __launch_bounds__(kThreads) k_pascal(int64_t n, double *__restrict__ zn) {
+    GRID_LOOP(i, n) {
+        double a[Q + 1];
+#pragma unroll
+        for (int j = 0; j <= Q; ++j) a[j] = zn[(int64_t)j * n + i];
+#pragma unroll
+        for (int k = 1; k <= Q; ++k)
+#pragma unroll
+            for (int j = Q; j >= k; --j) a[j - 1] = FWD ? a[j - 1] + a[j] : a[j - 1] - a[j];
+#pragma unroll
+        for (int j = 0; j < Q; ++j) zn[(int64_t)j * n + i] = a[j];
+    }
+}
+template <bool FWD>
+static void pascal(int64_t n, double *zn, int q, hipStream_t s) {
+    const int g = grid_blocks(n);
+    switch (q) {
+    case 1: k_pascal<1, FWD><<<g, kThreads, 0, s>>>(n, zn); break;
+    case 2: k_pascal<2, FWD><<<g, kThreads, 0, s>>>(n, zn); break;
+    case 3: k_pascal<3, FWD><<<g, kThreads, 0, s>>>(n, zn); break;
+    case 4: k_pascal<4, FWD><<<g, kThreads, 0, s>>>(n, zn); break;
+    default: k_pascal<5, FWD><<<g, kThreads, 0, s>>>(n, zn); break;
+    }
+}
+void predict(int64_t n, double *zn, int q, hipStream_t s) { pascal<true>(n, zn, q, s); }
+void restore(int64_t n, double *zn, int q, hipStream_t s) { pascal<false>(n, zn, q, s); }
+
+// cvRescale: zn[j] *= eta^j (N_VScaleVectorArray).  16*q B/entry.
+__global__ void __launch_bounds__(kThreads) k_rescale(int64_t n, double *__restrict__ zn, int q, Coefs c) {
+    GRID_LOOP(i, n) {
+        for (int j = 1; j <= q; ++j) zn[(int64_t)j * n + i] *= c.c[j];
+    }
+}
+void rescale(int64_t n, double *zn, int q, const Coefs &c, hipStream_t s) {
+    k_rescale<<<grid_blocks(n), kThreads, 0, s>>>(n, zn, q, c);
+}
+
+__global__ void __launch_bounds__(kThreads) k_vsum(int64_t n, const double *__restrict__ x, const double *__restrict__ y,
+                                                   double *__restrict__ z) {
+    GRID_LOOP(i, n) z[i] = x[i] + y[i];
+}
+void vsum(int64_t n, const double *x, const double *y, double *z, hipStream_t s) {
+    k_vsum<<<grid_blocks(n), kThreads, 0, s>>>(n, x, y, z);
+}
+
+__global__ void __launch_bounds__(kThreads) k_scale_to(int64_t n, double c, const double *x, double *z) {
+    GRID_LOOP(i, n) z[i] = c * x[i];
+}
+void scale_to(int64_t n, double c, const double *x, double *z, hipStream_t s) {
+    k_scale_to<<<grid_blocks(n), kThreads, 0, s>>>(n, c, x, z);
+}
+void copy(int64_t n, const double *x, double *z, hipStream_t s) {
+    (void)hipMemcpyAsync(z, x, n * sizeof(double), hipMemcpyDeviceToDevice, s);
+}
+void zero(int64_t n, double *z, hipStream_t s) { (void)hipMemsetAsync(z, 0, n * sizeof(double), s); }
+
+// cvIncreaseBDF / cvDecreaseBDF: zn[j] = coef[j]*zn[src] + zn[j] (N_VScaleAddMulti / Vaxpy)
+__global__ void __launch_bounds__(kThreads) k_axpy_multi(int64_t n, double *__restrict__ zn, int src, Coefs c, int jlo,
+                                                         int jhi) {
+    GRID_LOOP(i, n) {
+        const double x = zn[(int64_t)src * n + i];
+        for (int j = jlo; j <= jhi; ++j) zn[(int64_t)j * n + i] = c.c[j] * x + zn[(int64_t)j * n + i];
+    }
+}
+void axpy_multi(int64_t n, double *zn, int src, const Coefs &coef, int jlo, int jhi, hipStream_t s) {
+    if (jhi < jlo) return;
+    k_axpy_multi<<<grid_blocks(n), kThreads, 0, s>>>(n, zn, src, coef, jlo, jhi);
+}
+
+// cvNlsResidual (res = rl1*zn[1] + ycor; res += (-gamma)*ftemp) + Newton's N_VScale(-1, delta, delta)
+// + cvLsSolve's N_VWrmsNorm(b, ewt) (= SPGMR's ||s1*b||_2 / sqrt(N)).  40 B/entry.
+__global__ void __launch_bounds__(kThreads) k_residual(int64_t n, const double *__restrict__ zn1,
+                                                       const double *__restrict__ ycor, const double *__restrict__ ftemp,
+                                                       double rl1, double ngamma, const double *__restrict__ ewt,
+                                                       double *__restrict__ delta, Red r) {
+    double v[1] = {0.0};
+    GRID_LOOP(i, n) {
+        const double r1 = rl1 * zn1[i] + ycor[i];
+        const double r2 = r1 + ngamma * ftemp[i];
+        const double d = -r2;
+        delta[i] = d;
+        const double p = d * ewt[i];
+        v[0] += p * p;
+    }
+    block_partial<1>(v, 0u, r);
+}
+void residual(int64_t n, const double *zn1, const double *ycor, const double *ftemp, double rl1, double ngamma,
+              const double *ewt, double *delta, const Red &r, hipStream_t s) {
+    k_residual<<<r.nblk, kThreads, 0, s>>>(n, zn1, ycor, ftemp, rl1, ngamma, ewt, delta, r);
+}
+
+// SPGMR: vtemp = s1*r0; V[0] = (1/r_norm)*vtemp; and the WRMS norm of V[0]/s2 for the first DQ perturbation.
+__global__ void __launch_bounds__(kThreads) k_krylov_v0(int64_t n, const double *__restrict__ delta,
+                                                        const double *__restrict__ ewt, double c,
+                                                        double *__restrict__ V0, Red r) {
+    double v[1] = {0.0};
+    GRID_LOOP(i, n) {
+        const double w = ewt[i];
+        const double x = c * (w * delta[i]);
+        V0[i] = x;
+        const double p = (x / w) * w;
+        v[0] += p * p;
+    }
+    block_partial<1>(v, 0u, r);
+}
+void krylov_v0(int64_t n, const double *delta, const double *ewt, double c, double *V0, const Red &r, hipStream_t s) {
+    k_krylov_v0<<<r.nblk, kThreads, 0, s>>>(n, delta, ewt, c, V0, r);
+}
+
+__device__ inline double dq_sig(const double *ds, int64_t n) { return 1.0 / sqrt(ds[S_SIG] / (double)n); }
+
+// cvLsDQJtimes: work = sig*v + y with v = V[l]/s2 (N_VDiv) and sig = 1/||v||_wrms.  32 B/entry.
+__global__ void __launch_bounds__(kThreads) k_dq_work(int64_t n, const double *__restrict__ V,
+                                                      const double *__restrict__ ewt, const double *__restrict__ y,
+                                                      double *__restrict__ work, const double *__restrict__ ds) {
+    const double sig = dq_sig(ds, n);
+    GRID_LOOP(i, n) work[i] = sig * (V[i] / ewt[i]) + y[i];
+}
+void dq_work(int64_t n, const double *V, const double *ewt, const double *y, double *work, const double *ds,
+             hipStream_t s) {
+    k_dq_work<<<grid_blocks(n), kThreads, 0, s>>>(n, V, ewt, y, work, ds);
+}
+
+// cvLsDQJtimes tail (Jv = siginv*(f(work) - fy)), cvLsATimes (z = v - gamma*Jv), SPGMR left scaling
+// (V[l+1] = s1*z), and the first two Gram-Schmidt reductions (||V[l+1]||^2, V[0].V[l+1]).  48 B/entry.
+__global__ void __launch_bounds__(kThreads) k_atimes(int64_t n, double *__restrict__ w, const double *__restrict__ fy,
+                                                     const double *__restrict__ V, const double *__restrict__ ewt,
+                                                     const double *__restrict__ V0, double ngamma,
+                                                     const double *__restrict__ ds, Red r) {
+    const double sig = dq_sig(ds, n);
+    const double siginv = 1.0 / sig;
+    double v[2] = {0.0, 0.0};
+    GRID_LOOP(i, n) {
+        const double e = ewt[i];
+        const double jv = siginv * (w[i] - fy[i]);
+        const double z = ngamma * jv + V[i] / e;
+        const double x = e * z;
+        w[i] = x;
+        v[0] += x * x;
+        v[1] += V0[i] * x;
+    }
+    block_partial<2>(v, 0u, r);
+}
+void atimes(int64_t n, double *w, const double *fy, const double *V, const double *ewt, const double *V0,
+            double ngamma, const double *ds, const Red &r, hipStream_t s) {
+    k_atimes<<<r.nblk, kThreads, 0, s>>>(n, w, fy, V, ewt, V0, ngamma, ds, r);
+}
+
+// SUNModifiedGS step: v[k] -= h[i-1] v[i-1] (N_VLinearSum -> Vaxpy), then h[i] = v[i].v[k] (or ||v[k]||^2).
+__global__ void __launch_bounds__(kThreads) k_mgs(int64_t n, double *__restrict__ w, const double *__restrict__ Vprev,
+                                                  const double *__restrict__ ds, int hslot,
+                                                  const double *__restrict__ Vnext, Red r) {
+    const double nh = Vprev ? -ds[hslot] : 0.0;
+    double v[1] = {0.0};
+    GRID_LOOP(i, n) {
+        double x = w[i];
+        if (Vprev) {
+            x = x + nh * Vprev[i];
+            w[i] = x;
+        }
+        v[0] += Vnext ? Vnext[i] * x : x * x;
+    }
+    block_partial<1>(v, 0u, r);
+}
+void mgs(int64_t n, double *w, const double *Vprev, const double *ds, int hslot, const double *Vnext, const Red &r,
+         hipStream_t s) {
+    k_mgs<<<r.nblk, kThreads, 0, s>>>(n, w, Vprev, ds, hslot, Vnext, r);
+}
+
+// SPGMR: V[l+1] *= 1/h[l+1][l]; and the WRMS norm of V[l+1]/s2 for the next DQ perturbation.  24 B/entry.
+__global__ void __launch_bounds__(kThreads) k_normalize(int64_t n, double *__restrict__ w, double c,
+                                                        const double *__restrict__ ewt, Red r) {
+    double v[1] = {0.0};
+    GRID_LOOP(i, n) {
+        const double x = w[i] * c;
+        w[i] = x;
+        const double e = ewt[i];
+        const double p = (x / e) * e;
+        v[0] += p * p;
+    }
+    block_partial<1>(v, 0u, r);
+}
+void normalize(int64_t n, double *w, double c, const double *ewt, const Red &r, hipStream_t s) {
+    k_normalize<<<r.nblk, kThreads, 0, s>>>(n, w, c, ewt, r);
+}
+
+// SPGMR solution xcor = sum_k yg[k] V[k] (N_VLinearCombination into xcor = 0), x = xcor/s2 (N_VDiv),
+// cvLsSolve's b = x, Newton's ycor += delta, and the convergence test's two WRMS norms.
+__global__ void __launch_bounds__(kThreads) k_newton_update(int64_t n, const double *__restrict__ V, int64_t vstride,
+                                                            int krydim, Coefs yg, const double *__restrict__ dsrc,
+                                                            const double *__restrict__ ewt,
+                                                            double *__restrict__ ycor, Red r) {
+    double v[2] = {0.0, 0.0};
+    GRID_LOOP(i, n) {
+        const double e = ewt[i];
+        double d;
+        if (krydim > 0) {
+            double xc = 0.0;
+            for (int k = 0; k < krydim; ++k) xc = xc + yg.c[k] * V[k * vstride + i];
+            d = xc / e;
+        } else {
+            d = dsrc ? dsrc[i] : 0.0;
+        }
+        const double yc = ycor[i] + d;
+        ycor[i] = yc;
+        const double p = d * e, q = yc * e;
+        v[0] += p * p;
+        v[1] += q * q;
+    }
+    block_partial<2>(v, 0u, r);
+}
+void newton_update(int64_t n, const double *V, int64_t vstride, int krydim, const Coefs &yg, const double *dsrc,
+                   const double *ewt, double *ycor, const Red &r, hipStream_t s) {
+    k_newton_update<<<r.nblk, kThreads, 0, s>>>(n, V, vstride, krydim, yg, dsrc, ewt, ycor, r);
+}
+
+// cvCompleteStep: zn[j] = l[j]*acor + zn[j] (N_VScaleAddMulti), optional zn[qmax] = acor.
+__global__ void __launch_bounds__(kThreads) k_complete(int64_t n, double *__restrict__ zn,
+                                                       const double *__restrict__ acor, Coefs l, int q, int copy_to) {
+    GRID_LOOP(i, n) {
+        const double a = acor[i];
+        for (int j = 0; j <= q; ++j) zn[(int64_t)j * n + i] = l.c[j] * a + zn[(int64_t)j * n + i];
+        if (copy_to >= 0) zn[(int64_t)copy_to * n + i] = a;
+    }
+}
+void complete_step(int64_t n, double *zn, const double *acor, const Coefs &l, int q, int copy_to, hipStream_t s) {
+    k_complete<<<grid_blocks(n), kThreads, 0, s>>>(n, zn, acor, l, q, copy_to);
+}
+
+// cvComputeEtaqm1 / cvComputeEtaqp1 norms in one pass
+__global__ void __launch_bounds__(kThreads) k_eta_norms(int64_t n, const double *__restrict__ znq,
+                                                        const double *__restrict__ znqmax,
+                                                        const double *__restrict__ acor, double ncquot,
+                                                        const double *__restrict__ ewt, Red r) {
+    double v[2] = {0.0, 0.0};
+    GRID_LOOP(i, n) {
+        const double e = ewt[i];
+        if (znq) {
+            const double p = znq[i] * e;
+            v[0] += p * p;
+        }
+        if (znqmax) {
+            const double t = ncquot * znqmax[i] + acor[i];
+            const double p = t * e;
+            v[1] += p * p;
+        }
+    }
+    block_partial<2>(v, 0u, r);
+}
+void eta_norms(int64_t n, const double *zn_q, const double *zn_qmax, const double *acor, double ncquot,
+               const double *ewt, const Red &r, hipStream_t s) {
+    k_eta_norms<<<r.nblk, kThreads, 0, s>>>(n, zn_q, zn_qmax, acor, ncquot, ewt, r);
+}
+
+// N_VLinearSum_Serial's case analysis for z distinct from x and y
+__device__ inline double lin_sum2(double a, double x, double b, double y) {
+    if (a == 1.0 && b == 1.0) return x + y;
+    if (a == 1.0 && b == -1.0) return x - y;
+    if (a == -1.0 && b == 1.0) return y - x;
+    if (a == 1.0) return (b * y) + x;
+    if (b == 1.0) return (a * x) + y;
+    if (a == -1.0) return (b * y) - x;
+    if (b == -1.0) return (a * x) - y;
+    if (a == b) return a * (x + y);
+    if (a == -b) return a * (x - y);
+    return (a * x) + (b * y);
+}
+
+struct Js {
+    int j[kQMax + 1];
+};
+
+// CVodeGetDky: N_VLinearCombination(nvec, c, zn[js], dky), then N_VScale(h^-k, dky, dky) for k > 0
+__global__ void __launch_bounds__(kThreads) k_dky(int64_t n, const double *__restrict__ zn, int64_t stride, Js js,
+                                                  Coefs c, int nvec, double rscale, double *__restrict__ out) {
+    GRID_LOOP(i, n) {
+        double z;
+        if (nvec == 1) {
+            z = c.c[0] * zn[js.j[0] * stride + i];
+        } else if (nvec == 2) {
+            z = lin_sum2(c.c[0], zn[js.j[0] * stride + i], c.c[1], zn[js.j[1] * stride + i]);
+        } else {
+            z = c.c[0] * zn[js.j[0] * stride + i];
+            for (int k = 1; k < nvec; ++k) z += c.c[k] * zn[js.j[k] * stride + i];
+        }
+        if (rscale != 0.0) z *= rscale;
+        out[i] = z;
+    }
+}
+void dky(int64_t n, const double *zn, int64_t stride, const int *jsv, const Coefs &c, int nvec, double rscale,
+         double *out, hipStream_t s) {
+    Js js{};
+    for (int k = 0; k < nvec && k <= kQMax; ++k) js.j[k] = jsv[k];
+    k_dky<<<grid_blocks(n), kThreads, 0, s>>>(n, zn, stride, js, c, nvec, rscale, out);
+}
+
+}  // namespace ode
+}  // namespace shud

@@ -137,6 +137,24 @@ class ShudEtOut(C.Structure):
     _fields_ = [(n, c_double_p) for n in ET_OUT]
 
 
+# ---- include/shud_ode.h (device-resident integrator) ----
+class ShudOdeOptions(C.Structure):
+    _fields_ = [("reltol", C.c_double), ("abstol", C.c_double), ("init_step", C.c_double), ("max_step", C.c_double),
+                ("min_step", C.c_double), ("max_num_steps", C.c_int64), ("maxl", C.c_int32), ("max_order", C.c_int32)]
+
+
+ODE_STATS_I = ["nst", "nfe", "nfe_ls", "nni", "ncfn", "nnf", "netf", "nsetups", "nli", "ncfl", "njtimes"]
+
+
+class ShudOdeStats(C.Structure):
+    _fields_ = ([(n, C.c_int64) for n in ODE_STATS_I] + [("qlast", C.c_int32), ("qcur", C.c_int32)] +
+                [(n, C.c_double) for n in ["hlast", "hcur", "tcur", "hnext"]] + [("n_sync", C.c_int64)])
+
+
+ODE_SUCCESS, ODE_TSTOP_RETURN, ODE_RHSFUNC_FAIL = 0, 1, -8
+ODE_NORMAL, ODE_ONE_STEP = 1, 2
+OdeRhsFn = C.CFUNCTYPE(C.c_int, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p)
+
 # functions declared in include/shud_rhs.h (name -> (restype, argtypes))
 _H = C.c_void_p
 FUNCTIONS = {
@@ -177,9 +195,22 @@ ET_FUNCTIONS = {
     "shud_et_get": (C.c_int, [_H, C.POINTER(ShudEtOut)]),
 }
 
+# include/shud_ode.h
+ODE_FUNCTIONS = {
+    "shud_ode_create": (C.c_int, [_H, C.c_double, C.c_void_p, C.c_int, C.POINTER(ShudOdeOptions), C.POINTER(_H)]),
+    "shud_ode_create_fn": (C.c_int, [C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_double, C.c_void_p, C.c_int,
+                                     C.POINTER(ShudOdeOptions), C.POINTER(_H)]),
+    "shud_ode_set_stop_time": (C.c_int, [_H, C.c_double]),
+    "shud_ode_solve": (C.c_int, [_H, C.c_double, C.c_void_p, C.c_int, C.POINTER(C.c_double), C.c_int]),
+    "shud_ode_get_dky": (C.c_int, [_H, C.c_double, C.c_int, C.c_void_p, C.c_int]),
+    "shud_ode_get_stats": (C.c_int, [_H, C.POINTER(ShudOdeStats)]),
+    "shud_ode_state_device": (C.c_void_p, [_H]),
+    "shud_ode_destroy": (C.c_int, [_H]),
+}
+
 
 def bind(lib):
-    for name, (res, args) in list(FUNCTIONS.items()) + list(ET_FUNCTIONS.items()):
+    for name, (res, args) in list(FUNCTIONS.items()) + list(ET_FUNCTIONS.items()) + list(ODE_FUNCTIONS.items()):
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args

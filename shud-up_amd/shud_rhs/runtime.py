@@ -209,3 +209,61 @@ def nccl_unique_id():
     buf = C.create_string_buffer(128)
     _check(lib().shud_rhs_nccl_unique_id(buf), "nccl_unique_id")
     return buf.raw
+
+
+class OdeSolver:
+    """Device-resident CVODE-semantics integrator (include/shud_ode.h) over an RhsHandle, or over a raw device
+    RHS function pointer (tests).  Mirrors SetCVODE (cvode_config.cpp:149-197) + CVode() as SHUD() calls it."""
+
+    def __init__(self, rhs, t0, y0, reltol, abstol, init_step, max_step=0.0, min_step=1e-6,
+                 max_num_steps=1000000, maxl=0, max_order=0, fn=None):
+        self._opt = abi.ShudOdeOptions(reltol, abstol, init_step, max_step, min_step, max_num_steps, maxl, max_order)
+        y0 = np.ascontiguousarray(y0, dtype=np.float64)
+        self.n = y0.size
+        h = C.c_void_p()
+        if fn is None:
+            self._rhs = rhs
+            if self.n != rhs.num_y:
+                raise ValueError(f"y0 has {self.n} entries, expected {rhs.num_y}")
+            _check(lib().shud_ode_create(rhs.h, float(t0), y0.ctypes.data, abi.SHUD_WHERE_HOST, C.byref(self._opt),
+                                         C.byref(h)), "shud_ode_create")
+        else:                                   # fn = (function pointer, user pointer, stream)
+            self._fn = fn
+            _check(lib().shud_ode_create_fn(self.n, fn[0], fn[1], fn[2], float(t0), y0.ctypes.data,
+                                            abi.SHUD_WHERE_HOST, C.byref(self._opt), C.byref(h)), "shud_ode_create_fn")
+        self.h = h
+
+    def set_stop_time(self, tstop):
+        lib().shud_ode_set_stop_time(self.h, float(tstop))
+
+    def solve(self, tout, one_step=False, y_out=True):
+        """CVode(mem, tout, y, &t, CV_NORMAL | CV_ONE_STEP) -> (flag, t, y or None)"""
+        y = np.empty(self.n) if y_out else None
+        t = C.c_double()
+        flag = lib().shud_ode_solve(self.h, float(tout), None if y is None else y.ctypes.data, abi.SHUD_WHERE_HOST,
+                                    C.byref(t), abi.ODE_ONE_STEP if one_step else abi.ODE_NORMAL)
+        return flag, t.value, y
+
+    def get_dky(self, t, k):
+        d = np.empty(self.n)
+        flag = lib().shud_ode_get_dky(self.h, float(t), int(k), d.ctypes.data, abi.SHUD_WHERE_HOST)
+        return flag, d
+
+    def stats(self):
+        s = abi.ShudOdeStats()
+        lib().shud_ode_get_stats(self.h, C.byref(s))
+        return {k: getattr(s, k) for k, _ in abi.ShudOdeStats._fields_}
+
+    def state_device(self):
+        return lib().shud_ode_state_device(self.h)
+
+    def close(self):
+        if self.h:
+            lib().shud_ode_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass

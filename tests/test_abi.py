@@ -1,4 +1,4 @@
-"""CPU: the C-ABI library loads and exports every function include/shud_rhs.h declares; ctypes mirrors
+"""CPU: the C-ABI library loads and exports every function include/*.h declares; ctypes mirrors
 match the header.  No compute calls (no GPU here)."""
 import ctypes as C
 import os
@@ -8,7 +8,8 @@ import subprocess
 from conftest import ROOT
 from shud_rhs import abi
 
-HEADERS = {"shud_rhs.h": ("shud_rhs_", abi.FUNCTIONS), "shud_et.h": ("shud_et_", abi.ET_FUNCTIONS)}
+HEADERS = {"shud_rhs.h": ("shud_rhs_", abi.FUNCTIONS), "shud_et.h": ("shud_et_", abi.ET_FUNCTIONS),
+           "shud_ode.h": ("shud_ode_", abi.ODE_FUNCTIONS)}
 LIB = os.path.join(ROOT, "shud-up_amd", "libshud_rhs.so")
 
 
@@ -41,7 +42,7 @@ def test_library_exports_every_symbol():
 
 
 def _c_sizeof(struct):
-    src = f'#include "shud_rhs.h"\n#include "shud_et.h"\n#include <stdio.h>\nint main(){{printf("%zu\\n", sizeof({struct}));return 0;}}\n'
+    src = f'#include "shud_rhs.h"\n#include "shud_et.h"\n#include "shud_ode.h"\n#include <stdio.h>\nint main(){{printf("%zu\\n", sizeof({struct}));return 0;}}\n'
     exe = f"/tmp/sz_{struct}_{os.getpid()}"
     subprocess.run(["gcc", "-x", "c", "-", "-I", os.path.join(ROOT, "include"), "-o", exe], input=src.encode(),
                    check=True)
@@ -56,5 +57,6 @@ def test_struct_layouts_match_header():
                       ("ShudFluxOut", abi.ShudFluxOut), ("ShudErr", abi.ShudErr),
                       ("ShudPartition", abi.ShudPartition), ("ShudEtMeshSoA", abi.ShudEtMeshSoA),
                       ("ShudEtParams", abi.ShudEtParams), ("ShudEtForcing", abi.ShudEtForcing),
-                      ("ShudEtOut", abi.ShudEtOut)]:
+                      ("ShudEtOut", abi.ShudEtOut), ("ShudOdeOptions", abi.ShudOdeOptions),
+                      ("ShudOdeStats", abi.ShudOdeStats)]:
         assert C.sizeof(cls) == _c_sizeof(name), name

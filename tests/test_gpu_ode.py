@@ -1,0 +1,192 @@
+"""GPU: the device-resident integrator (include/shud_ode.h) against the CPU restatement
+(oracle/shud_oracle_ode.c, CVODE 6.0.0 BDF/Newton/SPGMR as SetCVODE configures it).
+
+(1) IEEE-exact test RHS (Robertson, decay, n-component decay over many blocks): with the oracle's reductions in
+    the device's fixed order, every output and every counter is bit-identical — the fused device kernels
+    perform CVODE's N_Vector arithmetic exactly, and the host control makes the same decisions.
+(2) The SHUD RHS (ccw; the branch-variant mesh with the device ET prelude coupled as in SHUD()'s loop): device
+    RHS + device integrator vs oracle RHS + oracle integrator.  The RHS itself differs by OCML-vs-glibc ulps, so
+    states agree to a tolerance far below the solver's own (rtol 1e-4) and the step/order sequences match.
+(3) A physics error inside the integration surfaces as CV_RHSFUNC_FAIL and the reference exit code.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import cases
+import oracle
+from conftest import PKG_DIR
+from shud_rhs import abi, et, workload
+from shud_rhs import runtime as rt
+from shud_rhs.solver import ShudSolver, SolverControl
+
+pytestmark = pytest.mark.gpu
+
+COUNTERS = ["nst", "nfe", "nfe_ls", "nni", "ncfn", "nnf", "netf", "nsetups", "nli", "ncfl", "njtimes", "qlast",
+            "qcur", "hlast", "hcur", "tcur", "hnext"]
+
+
+@pytest.fixture(scope="module")
+def kat():
+    lib = C.CDLL(os.path.join(PKG_DIR, "libshud_kat.so"))
+    lib.shud_kat_ode_user.restype = C.c_void_p
+    lib.shud_kat_ode_user.argtypes = [C.c_int]
+    lib.shud_kat_ode_stream.restype = C.c_void_p
+    lib.shud_kat_ode_stream.argtypes = [C.c_void_p]
+    lib.shud_kat_ode_set_n.argtypes = [C.c_int64]
+    lib.shud_kat_ode_free.argtypes = [C.c_void_p]
+    rt.lib()
+    return lib
+
+
+@pytest.fixture
+def device_order():
+    oracle.OracleOde.set_reduction_order(1)
+    yield
+    oracle.OracleOde.set_reduction_order(0)
+
+
+def _dev(kat, problem, n):
+    u = kat.shud_kat_ode_user({"robertson": 1, "decay": 2, "decayn": 3}[problem])
+    kat.shud_kat_ode_set_n(n)
+    fn = C.cast(kat.shud_kat_ode_rhs, C.c_void_p).value
+    return u, (fn, u, kat.shud_kat_ode_stream(u))
+
+
+def _same_stats(a, b):
+    for k in COUNTERS:
+        assert a[k] == b[k], (k, a[k], b[k])
+
+
+@pytest.mark.parametrize("problem,n,rtol,atol,h0,touts", [
+    ("robertson", 3, 1e-6, 1e-12, 1e-6, [0.4, 4.0, 40.0, 400.0, 4e3, 4e4, 4e5]),
+    ("decay", 3, 1e-8, 1e-12, 1e-4, [0.1, 1.0, 5.0]),
+    ("decayn", 7 * 40000, 1e-6, 1e-10, 1e-5, [0.01, 1.0, 10.0]),
+])
+def test_device_integrator_bit_identical(kat, device_order, problem, n, rtol, atol, h0, touts):
+    y0 = np.array([1.0, 0.0, 0.0]) if problem == "robertson" else 1.0 + 0.5 * np.sin(np.arange(n))
+    u, fn = _dev(kat, problem, n)
+    d = rt.OdeSolver(None, 0.0, y0, rtol, atol, h0, 0.0, 0.0, fn=fn)
+    o = oracle.OracleOde(problem, 0.0, y0, rtol, atol, h0, 0.0, 0.0)
+    for tout in touts:
+        fd, td, yd = d.solve(tout)
+        fo, to, yo = o.solve(tout)
+        assert fd == fo == 0 and td == to == tout
+        assert np.array_equal(yd, yo), (tout, np.abs(yd - yo).max())
+    _same_stats(d.stats(), o.stats())
+    d.close()
+    kat.shud_kat_ode_free(u)
+
+
+def test_device_stop_time_one_step_dky(kat, device_order):
+    u, fn = _dev(kat, "decay", 3)
+    y0 = np.ones(3)
+    d = rt.OdeSolver(None, 0.0, y0, 1e-6, 1e-10, 1e-3, 0.0, 0.0, fn=fn)
+    o = oracle.OracleOde("decay", 0.0, y0, 1e-6, 1e-10, 1e-3, 0.0, 0.0)
+    for s in (d, o):
+        s.set_stop_time(0.25)
+    rd, ro = d.solve(1.0), o.solve(1.0)
+    assert rd[0] == ro[0] == abi.ODE_TSTOP_RETURN and rd[1] == ro[1] == 0.25 and np.array_equal(rd[2], ro[2])
+    for _ in range(5):
+        rd, ro = d.solve(1.0, one_step=True), o.solve(1.0, one_step=True)
+        assert rd[0] == ro[0] == 0 and rd[1] == ro[1] and np.array_equal(rd[2], ro[2])
+    for k in range(3):
+        for tt in [rd[1], rd[1] - 0.3 * d.stats()["hlast"]]:
+            (fd, dd), (fo, do) = d.get_dky(tt, k), o.get_dky(tt, k)
+            assert fd == fo
+            if fd == 0:
+                assert np.array_equal(dd, do), (k, tt)
+    assert d.get_dky(rd[1] + 5.0, 0)[0] == -25
+    _same_stats(d.stats(), o.stats())
+    d.close()
+    kat.shud_kat_ode_free(u)
+
+
+def _close_traj(yd, yo, what):
+    err = np.abs(yd - yo)
+    tol = 1e-9 * (np.abs(yo) + 1e-3)
+    assert np.all(err <= tol), f"{what}: max err {err.max():.3e} at {int(np.argmax(err / tol))}"
+
+
+@pytest.mark.parametrize("mode", [abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP])
+def test_shud_ccw_integration_vs_oracle(device_order, mode):
+    m, y0 = cases.ccw()
+    h = rt.RhsHandle(m, mode=mode)
+    h.set_step_inputs()
+    r = oracle.OracleRhs(m, mode)
+    r.set_step_inputs()
+    # ccw.cfg.para: ABSTOL 1e-4, RELTOL 1e-4, INIT_SOLVER_STEP 1, MAX_SOLVER_STEP 10; SetCVODE: min step 1e-6
+    d = rt.OdeSolver(h, 0.0, y0, 1e-4, 1e-4, 1.0, 10.0, 1e-6, 1000000)
+    o = oracle.OracleOde(r, 0.0, y0, 1e-4, 1e-4, 1.0, 10.0, 1e-6, 1000000)
+    for k in range(1, 19):                       # 3 hours of 10-minute solver steps (CV_NORMAL)
+        fd, td, yd = d.solve(10.0 * k)
+        fo, to, yo = o.solve(10.0 * k)
+        assert fd == fo == 0 and td == to
+        _close_traj(yd, yo, f"t={td}")
+    sd, so = d.stats(), o.stats()
+    for key in ["nst", "nfe", "nni", "nli", "netf", "ncfn", "qcur"]:
+        assert sd[key] == so[key], (key, sd[key], so[key])
+    assert h.num_calls() == sd["nfe"] + sd["nfe_ls"]       # every RHS call went through the device handle
+    d.close()
+    h.close()
+
+
+def test_shud_loop_with_device_et_vs_oracle(device_order):
+    """SHUD()'s loop (shud.cpp:89-131) with ET sub-stepping: per ET step the device prelude writes the step
+    inputs in place, then CVode(tout) with CVodeSetStopTime(tout); the oracle runs the same loop on the CPU."""
+    m, y0 = cases.variant(3000, seed=21)
+    etm = et.synth_et(m.num_ele, seed=6, terrain=True, lake_frac=0.0)
+    ctl = SolverControl(reltol=1e-4, abstol=1e-4, init_step=0.5, max_step=60.0, et_step=20.0)
+    assert ctl.et_substep
+    h = rt.RhsHandle(m, mode=abi.SHUD_MODE_SERIAL)
+    h.set_step_inputs()
+    h.et_attach(etm)
+    oe = oracle.OracleEt(etm)
+    r = oracle.OracleRhs(m)
+    r.set_step_inputs()
+
+    def forcing(t, tout):
+        return et.synth_forcing(t, tout - t, seed=int(t) + 1, tsr_mode=abi.SHUD_TSR_RECOMPUTE)
+
+    outs = []
+    sol = ShudSolver(h, y0, ctl)
+    sol.run(3, forcing=forcing, on_output=lambda i, t, y: outs.append((t, y.copy())))
+    # the oracle loop
+    o = oracle.OracleOde(r, 0.0, y0, ctl.reltol, ctl.abstol, ctl.init_step, ctl.max_step, ctl.min_step,
+                         ctl.max_num_steps)
+    t, tnext, k = 0.0, 0.0, 0
+    for i in range(3):
+        tnext += ctl.solver_step
+        while t + 1e-10 < tnext:
+            tout = min(t + ctl.et_step, tnext)
+            assert oe.step(forcing(t, tout)) == (0, -1)
+            # the oracle prelude's outputs feed the oracle RHS (the device prelude wrote the device handle's)
+            r.set_step_inputs(step=oe.step_inputs())
+            o.set_stop_time(tout)
+            flag, t, y = o.solve(tout)
+            assert flag == abi.ODE_TSTOP_RETURN
+        td, yd = outs[i]
+        assert td == t
+        # ET (OCML exp/log ulps) and the RHS ulps both enter here: tolerance 1e-7 relative
+        err = np.abs(yd - y)
+        assert np.all(err <= 1e-7 * (np.abs(y) + 1e-3)), err.max()
+    sd, so = sol.stats(), o.stats()
+    assert abs(sd["nst"] - so["nst"]) <= 1
+    sol.close()
+    h.close()
+
+
+def test_physics_error_surfaces():
+    m, y0 = cases.ccw()
+    y = y0.copy()
+    y[5] = np.nan                                   # NaN surface storage: the applyDY NaN check (exit 10)
+    h = rt.RhsHandle(m)
+    h.set_step_inputs()
+    d = rt.OdeSolver(h, 0.0, y, 1e-4, 1e-4, 1.0, 10.0)
+    flag, t, _ = d.solve(10.0)
+    assert flag == abi.ODE_RHSFUNC_FAIL
+    assert h.get_error()["exit_code"] == 10
+    d.close()
+    h.close()

@@ -1,0 +1,116 @@
+"""CPU: the integrator restatement (oracle/shud_oracle_ode.c, CVODE 6.0.0 BDF/Newton/SPGMR as SetCVODE configures
+it) against published known answers — SUNDIALS itself cannot run here, so these pin the restatement:
+
+* Robertson's stiff kinetics (Robertson 1966; the cvRoberts example problem of CVODE): against scipy's Radau
+  (an independent implicit Runge-Kutta code) at rtol 1e-12, at the outputs 0.4 ... 4e5 of cvRoberts_dns;
+* linear decay y_i' = -lambda_i y_i against exp(-lambda_i t), three rates and an n-component seven-rate system
+  whose Jacobian has more distinct eigenvalues than the Krylov dimension;
+* CVode's stop-time, one-step and dense-output (CVodeGetDky) contracts;
+* the SHUD RHS (ccw, serial) through the integrator: the solve finishes with sane statistics, and repeats
+  bit for bit (the stateful RHS and the integrator are deterministic).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from shud_rhs import ShudModel, workload
+
+from conftest import ROOT
+
+T_OUT = [0.4, 4.0, 40.0, 400.0, 4.0e3, 4.0e4, 4.0e5]
+
+
+def _robertson(t, y):
+    return [-0.04 * y[0] + 1e4 * y[1] * y[2], 0.04 * y[0] - 1e4 * y[1] * y[2] - 3e7 * y[1] ** 2, 3e7 * y[1] ** 2]
+
+
+@pytest.fixture(scope="module")
+def robertson_ref():
+    from scipy.integrate import solve_ivp
+    r = solve_ivp(_robertson, (0.0, T_OUT[-1]), [1.0, 0.0, 0.0], method="Radau", rtol=1e-12, atol=1e-20,
+                  t_eval=T_OUT)
+    assert r.success
+    return r.y.T
+
+
+def test_robertson_known_answer(robertson_ref):
+    o = oracle.OracleOde("robertson", 0.0, [1.0, 0.0, 0.0], 1e-6, 1e-12, 1e-6, 0.0, 0.0)
+    for k, tout in enumerate(T_OUT):
+        flag, t, y = o.solve(tout)
+        assert flag == 0 and t == tout
+        rel = np.abs(y - robertson_ref[k]) / np.abs(robertson_ref[k])
+        assert rel.max() < 5e-5, (tout, y, robertson_ref[k])
+        assert abs(y.sum() - 1.0) < 1e-9                         # mass conservation of the kinetics
+    st = o.stats()
+    assert st["qcur"] == 5 and st["netf"] > 0 and st["nst"] > 100
+    assert st["nfe"] == st["nni"] + 1 and st["nfe_ls"] == st["njtimes"] == st["nli"]
+
+
+def test_decay_known_answer():
+    lam = np.array([1.0, 10.0, 1000.0])
+    o = oracle.OracleOde("decay", 0.0, [1.0, 1.0, 1.0], 1e-8, 1e-12, 1e-4, 0.0, 0.0)
+    for tout in [0.1, 1.0, 5.0]:
+        flag, t, y = o.solve(tout)
+        ex = np.exp(-lam * tout)
+        assert flag == 0
+        assert np.all(np.abs(y - ex) <= 1e-6 * np.abs(ex) + 1e-10), (tout, y, ex)
+
+
+def test_decayn_more_modes_than_krylov_dim():
+    n = 7 * 300
+    lam = np.array([0.01, 0.1, 1.0, 10.0, 100.0, 1000.0, 10000.0])[np.arange(n) % 7]
+    y0 = 1.0 + 0.5 * np.sin(np.arange(n))
+    o = oracle.OracleOde("decayn", 0.0, y0, 1e-6, 1e-10, 1e-5, 0.0, 0.0)
+    for tout in [0.01, 1.0, 10.0]:
+        flag, t, y = o.solve(tout)
+        ex = y0 * np.exp(-lam * tout)
+        assert flag == 0
+        assert np.all(np.abs(y - ex) <= 2e-4 * np.abs(ex) + 1e-8), np.abs(y - ex).max()
+    st = o.stats()
+    assert st["nli"] > st["nni"] > 0
+
+
+def test_stop_time_one_step_and_dky():
+    o = oracle.OracleOde("decay", 0.0, [1.0, 1.0, 1.0], 1e-6, 1e-10, 1e-3, 0.0, 0.0)
+    o.set_stop_time(0.25)
+    flag, t, y = o.solve(1.0)
+    assert flag == 1 and t == 0.25                               # CV_TSTOP_RETURN at exactly tstop
+    assert abs(y[0] - np.exp(-0.25)) < 1e-5
+    flag, t1, y1 = o.solve(1.0, one_step=True)                   # one internal step past tstop
+    assert flag == 0 and 0.25 < t1 < 1.0
+    st = o.stats()
+    assert t1 == st["tcur"]
+    # dense output: zeroth derivative at tcur is the state, first is f(y) to the interpolation order
+    flag, d0 = o.get_dky(t1, 0)
+    assert flag == 0 and np.array_equal(d0, y1)
+    flag, d1 = o.get_dky(t1, 1)
+    assert flag == 0 and abs(d1[0] + y1[0]) < 1e-3 * abs(y1[0])
+    flag, _ = o.get_dky(t1 + 10.0, 0)
+    assert flag == -25                                           # CV_BAD_T outside [tcur - hu, tcur]
+
+
+def _ccw():
+    m = ShudModel.load(f"{ROOT}/tests/golden/ccw_model.npz")
+    y0 = np.load(f"{ROOT}/tests/golden/ccw_y0.npy")
+    m.step = workload.random_step_inputs(m, seed=11)
+    return m, y0
+
+
+def test_shud_rhs_through_integrator_deterministic():
+    m, y0 = _ccw()
+    outs = []
+    for rep in range(2):
+        r = oracle.OracleRhs(m)
+        r.set_step_inputs()
+        o = oracle.OracleOde(r, 0.0, y0, 1e-4, 1e-4, 1.0, 10.0, 1e-6, 1000000, 0)   # ccw.cfg.para settings
+        ys = []
+        for k in range(1, 7):
+            flag, t, y = o.solve(10.0 * k)
+            assert flag == 0 and t == 10.0 * k
+            assert np.all(np.isfinite(y))
+            ys.append(y)
+        outs.append((np.array(ys), o.stats()))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert outs[0][1] == outs[1][1]
+    st = outs[0][1]
+    assert st["nst"] >= 6 and st["hlast"] <= 10.0 and st["ncfn"] == 0
