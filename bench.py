@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--profile-reps", type=int, default=20)
     ap.add_argument("--host-vectors", action="store_true", help="also time the PCIe-inclusive host-vector eval")
     ap.add_argument("--no-et", action="store_true", help="skip the ET-step prelude timing (SURVEY f1)")
+    ap.add_argument("--no-ode", action="store_true", help="skip the device integrator timing (SURVEY f2)")
     ap.add_argument("--partition-1", action="store_true",
                     help="run the N>1 code path (partitioned handle, RCCL comm, overlap) with one rank (smoke test)")
     args = ap.parse_args()
@@ -191,6 +192,8 @@ def main():
 
     if world == 1 and not args.no_et:
         out["et_prelude"] = et_prelude_timing(h, gm)
+    if world == 1 and not args.no_ode:
+        out["integrator"] = ode_timing(h, y_glob, ms_eval)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(gm, y_glob, mode, args.cpu_seconds)
@@ -201,6 +204,33 @@ def main():
     h.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def ode_timing(h, y0, ms_eval, max_steps=40, budget_s=4.0):
+    """The device integrator (shud_ode_solve, SURVEY §8f f2: CVODE BDF/Newton/SPGMR as SetCVODE configures it,
+    ccw's cfg.para tolerances) on the same mesh and handle: internal steps (CV_ONE_STEP) from the bench state,
+    y never leaving HBM.  rhs_share = RHS evaluations x the RHS time measured above / wall time: the rest is
+    the fused N_Vector kernels plus the host's scalar control (one small D2H per Newton/Krylov iteration)."""
+    from shud_rhs.runtime import OdeSolver
+    ode = OdeSolver(h, 0.0, y0, 1e-4, 1e-4, 1e-2, 30.0)
+    flag, _, _ = ode.solve(1e9, one_step=True, y_out=False)        # first step: setup outside the timing
+    s0 = ode.stats()
+    n, t0 = 0, time.perf_counter()
+    while flag >= 0 and n < max_steps and time.perf_counter() - t0 < budget_s:
+        flag, _, _ = ode.solve(1e9, one_step=True, y_out=False)
+        n += 1
+    wall = time.perf_counter() - t0
+    s1 = ode.stats()
+    ode.close()
+    d = {k: s1[k] - s0[k] for k in ("nst", "nfe", "nfe_ls", "nni", "nli", "netf", "ncfn", "n_sync")}
+    nrhs = d["nfe"] + d["nfe_ls"]
+    return {"flag": flag, "steps": d["nst"], "rhs_evals": nrhs, "newton_iters": d["nni"], "krylov_iters": d["nli"],
+            "host_syncs": d["n_sync"], "ms_per_step": wall / max(1, d["nst"]) * 1e3,
+            "ms_per_rhs_eval_incl_solver": wall / max(1, nrhs) * 1e3,
+            "rhs_share": nrhs * ms_eval * 1e-3 / wall if wall > 0 else None,
+            "t_reached_min": s1["tcur"], "order": s1["qcur"], "h_min": s1["hcur"],
+            "note": "CV_ONE_STEP internal steps from the bench state (reltol 1e-4, abstol 1e-4, InitStep 1e-2, "
+                    "MaxStep 30 min), serial-semantics RHS, state in HBM"}
 
 
 def et_prelude_timing(h, gm, reps=10):
