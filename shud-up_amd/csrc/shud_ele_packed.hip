@@ -79,8 +79,11 @@ constexpr int CF_LDS_STRIDE = CF_COUNT | 1;
 // fun_Ele_lakeVertical / fun_Ele_lakeHorizon (Element.cpp:336-346, MD_ElementFlux.cpp:2-23) and get zero DY
 // (MD_f.cpp:146-150); bank edges of other elements exchange with the lake (MD_ElementFlux.cpp:46-53,107-121)
 // and leave their fluxes in DevLake for the lake kernel.  LAKE = false compiles all of it away.
+#ifndef SHUD_ELE_WAVES
+#define SHUD_ELE_WAVES 5        // min waves per SIMD: <= 96 VGPRs (rolled edge loop, no spills)
+#endif
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
-__global__ void __launch_bounds__(256, 5)
+__global__ void __launch_bounds__(256, SHUD_ELE_WAVES)
 shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int i0, int n_compute, int cur,
                        DevDiag dg, DevLake lk) {
     extern __shared__ double lct[];                       // ncls * CF_LDS_STRIDE doubles when LCT

@@ -72,6 +72,9 @@ struct shud_rhs {
     int tab_len[4] = {0, 0, 0, 0};
 
     EtState *et = nullptr;               // ET-step prelude (shud_et_attach), owned
+    // output path (shud_out.h): Model_Data::summary arrays and the derived ET sums, allocated on first use
+    double *d_sum[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};   // yEleSurf/Unsat/GW, yRivStg, yLakeStg
+    double *d_trans = nullptr, *d_evapo = nullptr;                      // qEleTrans, qEleEvapo
 
     DevErr *d_err = nullptr;
     DevErr *h_err = nullptr;             // pinned
@@ -115,4 +118,5 @@ struct shud_rhs {
 };
 
 int shud_reset_err(shud_rhs *h);
+int shud_diag_replay(shud_rhs *h);       // shud_rhs.cpp: last eval again with diagnostic stores (device only)
 void shud_et_free(shud_rhs *h);          // shud_et.cpp

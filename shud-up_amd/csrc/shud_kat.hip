@@ -40,6 +40,30 @@ __global__ void kat_kernel(int fn, int k, const double *__restrict__ in, int n, 
     out[t] = r;
 }
 
+// pow_pos (shud_physics.h) next to OCML's full pow on the same (x, y) pairs: which = 0 pow, 1 pow_pos
+__global__ void kat_pow_kernel(int which, const double *__restrict__ xy, int n, double *__restrict__ out) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const double x = xy[2 * t], y = xy[2 * t + 1];
+    out[t] = which ? pow_pos(x, y) : pow(x, y);
+}
+extern "C" int shud_kat_pow(int which, const double *h_xy, int n, double *h_out) {
+    if (n <= 0) return -1;
+    double *d_xy = nullptr, *d_out = nullptr;
+    if (hipMalloc(&d_xy, sizeof(double) * 2 * (size_t)n) != hipSuccess) return -3;
+    if (hipMalloc(&d_out, sizeof(double) * (size_t)n) != hipSuccess) { (void)hipFree(d_xy); return -3; }
+    int rc = 0;
+    if (hipMemcpy(d_xy, h_xy, sizeof(double) * 2 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess) rc = -3;
+    if (!rc) {
+        hipLaunchKernelGGL(kat_pow_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, which, d_xy, n, d_out);
+        if (hipGetLastError() != hipSuccess) rc = -3;
+    }
+    if (!rc && hipMemcpy(h_out, d_out, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess) rc = -3;
+    (void)hipFree(d_xy);
+    (void)hipFree(d_out);
+    return rc;
+}
+
 extern "C" int shud_kat_nin(int fn) { return (fn >= 0 && fn < KAT_COUNT) ? kat_nin_tab[fn] : -1; }
 
 extern "C" int shud_kat_eval(int fn, const double *h_in, int n, double *h_out) {

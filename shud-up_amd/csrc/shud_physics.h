@@ -162,9 +162,38 @@ __device__ __forceinline__ RivGeom riv_geom(double w0, double bs, double len, do
     g.toparea = (ta < 0.) ? 0. : ta;
     return g;
 }
-// satKfun, Equations.cpp:136-141, with the class exponents ex1 = n/(n-1), ex2 = (n-1)/n precomputed
+// pow(x, y) for a positive finite base and a finite exponent whose product y*ln(x) cannot overflow: OCML's
+// own pow core (__ocml_pow_f64, ocml.bc: extended-precision log, the two-product, extended exp) without the
+// ~30 selects that handle negative/zero/infinite/NaN bases, integer exponents and infinities.  On that domain
+// every special-case select of __ocml_pow_f64 passes the core's value through, so the result is the same
+// bits (tests/test_kat.py::test_pow_pos_bit_identical); x = 1 gives exp(y*0) = 1 exactly, as pow does.
+typedef double shud_v2d __attribute__((ext_vector_type(2)));
+extern "C" __device__ shud_v2d __ocmlpriv_epln_f64(double);
+extern "C" __device__ double __ocmlpriv_expep_f64(shud_v2d);
+__device__ __forceinline__ double pow_pos(double x, double y) {
+    const shud_v2d l = __ocmlpriv_epln_f64(x);          // ln x = l.y + l.x (head, tail)
+    const double hi = y * l.y;
+    const double lo = __builtin_fma(y, l.x, __builtin_fma(y, l.y, -hi));
+    const double s = hi + lo;
+    shud_v2d a;
+    a.y = s;
+    a.x = lo - (s - hi);
+    return __ocmlpriv_expep_f64(a);
+}
+#ifndef SHUD_POWPOS
+#define SHUD_POWPOS 1
+#endif
+#if SHUD_POWPOS && !(SHUD_ABL & 1)
+#define SPOW_SAT(a, b) pow_pos(a, b)
+#else
+#define SPOW_SAT(a, b) SPOW(a, b)
+#endif
+
+// satKfun, Equations.cpp:136-141, with the class exponents ex1 = n/(n-1), ex2 = (n-1)/n precomputed.
+// Both bases are positive here: satn in (ZERO, 0.99] (the callers' clamps), 1 - satn^ex1 in (0, 1];
+// exponents are class constants of Beta > 1 (checked by the handle) -> pow_pos
 __device__ __forceinline__ double sat_kfun(double satn, double ex1, double ex2) {
-    const double tmp = -1. + SPOW(1. - SPOW(satn, ex1), ex2);
+    const double tmp = -1. + SPOW_SAT(1. - SPOW_SAT(satn, ex1), ex2);
     return SSQRT(satn) * tmp * tmp;
 }
 // SoilMoistureStress, is_sm_et.cpp:131-140 (truncated PI), with dth = ThetaS - ThetaR and

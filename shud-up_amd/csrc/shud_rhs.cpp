@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -362,6 +363,9 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         t[CF_dTh] = t[CF_ThetaS] - t[CF_ThetaR];
         t[CF_ex1] = t[CF_Beta] / (t[CF_Beta] - 1.);
         t[CF_ex2] = (t[CF_Beta] - 1.) / t[CF_Beta];
+        // the packed kernel's satKfun uses pow_pos (positive bases, finite exponents: shud_physics.h);
+        // any other Beta keeps the SoA layout, whose kernel calls the full pow
+        if (!(t[CF_Beta] > 1.) || !std::isfinite(t[CF_ex1]) || !std::isfinite(t[CF_ex2])) return 0;
         t[CF_vb] = 1. - t[CF_VegFrac];
         t[CF_pj] = 1. - t[CF_ImpAF];
         t[CF_omh] = 1. - t[CF_hAreaF];
@@ -891,15 +895,22 @@ static int ensure_diag(shud_rhs *h) {
     return 0;
 }
 
-extern "C" int shud_rhs_sync_diagnostics(shud_rhs_t h, ShudFluxOut *o) {
-    if (!h || !o) return shud_fail(SHUD_ERR_ARG, "null argument");
+// replay of the last evaluation with diagnostic stores: same y, same carried-state inputs (it rewrites the
+// same carried outputs), ydot into scratch; stream-ordered, the diagnostics stay in HBM (DevDiag)
+int shud_diag_replay(shud_rhs *h) {
     if (!h->have_last) return shud_fail(SHUD_ERR_ARG, "no evaluation to report diagnostics for");
     HIP_TRY(hipSetDevice(h->device));
     int rc = ensure_diag(h);
     if (rc) return rc;
-    // replay: same y, same carried-state inputs; it rewrites the same carried outputs
     launch_all(h, h->last_y, h->d_scratch_dy, h->last_cur, h->last_cur_e, true);
     HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+extern "C" int shud_rhs_sync_diagnostics(shud_rhs_t h, ShudFluxOut *o) {
+    if (!h || !o) return shud_fail(SHUD_ERR_ARG, "null argument");
+    int rc = shud_diag_replay(h);
+    if (rc) return rc;
     const size_t NE = h->NE, NR = h->NR, NS = h->NS;
     auto get = [&](double *dst, const double *src, size_t n) -> int {
         if (dst && n) HIP_TRY(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToHost, h->stream));

@@ -208,9 +208,36 @@ ODE_FUNCTIONS = {
     "shud_ode_destroy": (C.c_int, [_H]),
 }
 
+# ---- include/shud_out.h (output path on the device) ----
+(SHUD_ARR_Y_ELE_SURF, SHUD_ARR_Y_ELE_UNSAT, SHUD_ARR_Y_ELE_GW, SHUD_ARR_Y_RIV_STG, SHUD_ARR_Y_LAKE_STG,
+ SHUD_ARR_QELE_SURF_TOT, SHUD_ARR_QELE_SUB_TOT, SHUD_ARR_QELE_SURF, SHUD_ARR_QELE_SUB, SHUD_ARR_QE2R_SURF,
+ SHUD_ARR_QE2R_SUB, SHUD_ARR_Q_INFIL, SHUD_ARR_Q_EXFIL, SHUD_ARR_Q_RECHARGE, SHUD_ARR_Q_ETA, SHUD_ARR_Q_E_IC,
+ SHUD_ARR_Q_TRANS, SHUD_ARR_Q_EVAPO, SHUD_ARR_QRIV_DOWN, SHUD_ARR_QRIV_UP, SHUD_ARR_QRIV_SURF, SHUD_ARR_QRIV_SUB,
+ SHUD_ARR_Q_PRCP, SHUD_ARR_Q_NET_PRCP, SHUD_ARR_Q_ETP, SHUD_ARR_COUNT) = range(26)
+
+
+class ShudPrintSpec(C.Structure):
+    _fields_ = [("basename", C.c_char_p), ("d_src", C.c_void_p), ("n_all", C.c_int32), ("flag_io", C.c_void_p),
+                ("interval", C.c_int32), ("iflux", C.c_int32), ("start_time", C.c_int64), ("binary", C.c_int32),
+                ("ascii", C.c_int32), ("radiation_input_mode", C.c_int32), ("terrain_radiation", C.c_int32),
+                ("solar_lonlat_mode", C.c_char_p), ("solar_lon_deg", C.c_double), ("solar_lat_deg", C.c_double)]
+
+
+OUT_FUNCTIONS = {
+    "shud_rhs_summary": (C.c_int, [_H, C.c_void_p]),
+    "shud_rhs_refresh_diagnostics": (C.c_int, [_H]),
+    "shud_rhs_device_array": (C.c_void_p, [_H, C.c_int, C.POINTER(C.c_int64)]),
+    "shud_out_create": (C.c_int, [C.c_int, C.c_void_p, C.POINTER(_H)]),
+    "shud_out_add": (C.c_int, [_H, C.POINTER(ShudPrintSpec)]),
+    "shud_out_export": (C.c_int, [_H, C.c_double]),
+    "shud_out_rows": (C.c_int64, [_H, C.c_int]),
+    "shud_out_destroy": (C.c_int, [_H]),
+}
+
 
 def bind(lib):
-    for name, (res, args) in list(FUNCTIONS.items()) + list(ET_FUNCTIONS.items()) + list(ODE_FUNCTIONS.items()):
+    for name, (res, args) in (list(FUNCTIONS.items()) + list(ET_FUNCTIONS.items()) + list(ODE_FUNCTIONS.items())
+                              + list(OUT_FUNCTIONS.items())):
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args

@@ -164,6 +164,20 @@ class RhsHandle:
         nm = names.value.decode().split(",")
         return ms_eval.value, {nm[k]: ms[k] for k in range(nk.value)}
 
+    # ---- output path (include/shud_out.h) ----
+    def summary(self, d_y):
+        """Model_Data::summary(udata) on the device: SHUD_ARR_Y_* from the state at d_y"""
+        _check(lib().shud_rhs_summary(self.h, C.c_void_p(d_y)), "summary")
+
+    def refresh_diagnostics(self):
+        """the last RHS evaluation replayed with diagnostic stores into the device arrays (no host copy)"""
+        _check(lib().shud_rhs_refresh_diagnostics(self.h), "refresh_diagnostics")
+
+    def device_array(self, which):
+        n = C.c_int64()
+        p = lib().shud_rhs_device_array(self.h, int(which), C.byref(n))
+        return p, n.value
+
     # ---- external-transport partition hooks ----
     def halo_buffers(self):
         p = [C.c_void_p() for _ in range(4)]
@@ -244,6 +258,13 @@ class OdeSolver:
                                     C.byref(t), abi.ODE_ONE_STEP if one_step else abi.ODE_NORMAL)
         return flag, t.value, y
 
+    def solve_device(self, tout, d_y, one_step=False):
+        """CVode() with y(t) written to device memory at d_y (NY doubles): -> (flag, t)"""
+        t = C.c_double()
+        flag = lib().shud_ode_solve(self.h, float(tout), C.c_void_p(d_y), abi.SHUD_WHERE_DEVICE, C.byref(t),
+                                    abi.ODE_ONE_STEP if one_step else abi.ODE_NORMAL)
+        return flag, t.value
+
     def get_dky(self, t, k):
         d = np.empty(self.n)
         flag = lib().shud_ode_get_dky(self.h, float(t), int(k), d.ctypes.data, abi.SHUD_WHERE_HOST)
@@ -260,6 +281,46 @@ class OdeSolver:
     def close(self):
         if self.h:
             lib().shud_ode_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class Output:
+    """The reference's Print_Ctrl set (Control_Data::ExportResults, Model_Control.cpp:123-127) with its buffers
+    in HBM (include/shud_out.h): add() = Print_Ctrl::Init[IJ] + open_file, export(t) = ExportResults(t)."""
+
+    def __init__(self, device=0, stream=None):
+        h = C.c_void_p()
+        _check(lib().shud_out_create(int(device), None if stream is None else C.c_void_p(stream), C.byref(h)),
+               "shud_out_create")
+        self.h = h
+        self._keep = []
+
+    def add(self, basename, d_src, n_all, interval, iflux, start_time=0, flag_io=None, binary=True, ascii=False,
+            radiation_input_mode=0, terrain_radiation=0, solar_lonlat_mode="FORCING_FIRST", lon=0.0, lat=0.0):
+        flags = None if flag_io is None else np.ascontiguousarray(flag_io, dtype=np.int32)
+        bn, sm = str(basename).encode(), str(solar_lonlat_mode).encode()
+        spec = abi.ShudPrintSpec(bn, C.c_void_p(d_src), int(n_all), None if flags is None else flags.ctypes.data,
+                                 int(interval), int(iflux), int(start_time), int(bool(binary)), int(bool(ascii)),
+                                 int(radiation_input_mode), int(terrain_radiation), sm, float(lon), float(lat))
+        _check(lib().shud_out_add(self.h, C.byref(spec)), "shud_out_add")
+        self._keep.append((bn, sm, flags))
+        return len(self._keep) - 1
+
+    def export(self, t):
+        _check(lib().shud_out_export(self.h, float(t)), "shud_out_export")
+
+    def rows(self, k):
+        return lib().shud_out_rows(self.h, int(k))
+
+    def close(self):
+        if self.h:
+            lib().shud_out_destroy(self.h)
             self.h = None
 
     def __del__(self):

@@ -239,3 +239,20 @@ def load_project(indir, prj, end_override=None):
         y0 = np.concatenate(parts)
     m.meta.update(prj=prj, x=ext["x"], y=ext["y"], raised=ext["raised"], close_boundary=close_boundary)
     return m, {"y0": y0, "S": S, "G": G, "L": L, "R": R, "calib": g, "att": att}
+
+
+def read_dat(path):
+    """Read a SHUD binary output file as Print_Ctrl writes it (src/classes/Model_Control.cpp:727-735, 893-899):
+    a 1024-byte text header, StartTime and NumVar as doubles, icol[NumVar] (1-based column ids as doubles),
+    then rows of (t, value[NumVar]) doubles, t = left endpoint of the output interval [min]."""
+    raw = np.fromfile(path, dtype=np.uint8)
+    header = raw[:1024].tobytes().split(b"\0", 1)[0].decode()
+    body = raw[1024:].view(np.float64)
+    start_time, nvar = body[0], int(body[1])
+    icol = body[2:2 + nvar].astype(np.int64)
+    rows = body[2 + nvar:]
+    if rows.size % (nvar + 1):
+        raise ValueError(f"{path}: {rows.size} values do not fill rows of {nvar + 1}")
+    rows = rows.reshape(-1, nvar + 1)
+    return {"header": header, "start_time": start_time, "icol": icol, "t": rows[:, 0].copy(),
+            "data": rows[:, 1:].copy()}

@@ -10,6 +10,8 @@ SolverStep = MaxStep, NumSteps = (END - START)/SolverStep, ET sub-stepping when 
 """
 from dataclasses import dataclass
 
+import numpy as np
+
 from . import abi
 from .runtime import OdeSolver, ShudRhsError
 
@@ -48,10 +50,15 @@ class ShudSolver:
                              ctl.min_step, ctl.max_num_steps)
         self.y = None
 
-    def run(self, num_steps, forcing=None, on_output=None):
-        """num_steps solver steps (the reference's NumSteps loop); on_output(i, t, y) after each."""
+    def run(self, num_steps, forcing=None, on_output=None, output=None):
+        """num_steps solver steps (the reference's NumSteps loop); on_output(i, t, y) after each (host copy of y).
+        output: runtime.Output whose controls point at the handle's device arrays — after each solver step
+        summary(udata) + ExportResults(t) run on the device (shud.cpp:137,153): no host copy of y at all."""
         ctl = self.ctl
         tnext = self.t
+        d_y = None
+        if output is not None:
+            d_y = self._out_y = getattr(self, "_out_y", None) or self.h.device_alloc(8 * self.h.num_y)
         for i in range(num_steps):
             tnext += ctl.solver_step
             while self.t + ZERO < tnext:
@@ -62,7 +69,11 @@ class ShudSolver:
                         self.h.et_step(f)
                 if ctl.et_substep:
                     self.ode.set_stop_time(tout)
-                flag, t, y = self.ode.solve(tout)
+                if d_y is not None:
+                    flag, t = self.ode.solve_device(tout, d_y)
+                    y = None
+                else:
+                    flag, t, y = self.ode.solve(tout)
                 if flag < 0:
                     if flag == abi.ODE_RHSFUNC_FAIL:
                         e = self.h.get_error()
@@ -70,7 +81,16 @@ class ShudSolver:
                             raise ShudRhsError(abi.SHUD_ERR_PHYSICS, e["message"], e)
                     raise RuntimeError(f"CVode failed with flag {flag} at t={t}")
                 self.t, self.y = t, y
+            if output is not None:
+                # Model_Data::summary(udata) on y(tout); the flux arrays are those of CVODE's last f() call,
+                # replayed on its input buffer (the integrator never rewrites that buffer before its next RHS
+                # call: the Newton residual's y and the DQ work vector are only written right before an RHS)
+                self.h.summary(d_y)
+                self.h.refresh_diagnostics()
+                output.export(self.t)
             if on_output is not None:
+                if self.y is None:
+                    self.y = self.h.d2h(np.empty(self.h.num_y), d_y)
                 on_output(i, self.t, self.y)
         return self.t, self.y
 
@@ -79,3 +99,6 @@ class ShudSolver:
 
     def close(self):
         self.ode.close()
+        if getattr(self, "_out_y", None):
+            self.h.device_free(self._out_y)
+            self._out_y = None

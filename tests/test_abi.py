@@ -9,7 +9,7 @@ from conftest import ROOT
 from shud_rhs import abi
 
 HEADERS = {"shud_rhs.h": ("shud_rhs_", abi.FUNCTIONS), "shud_et.h": ("shud_et_", abi.ET_FUNCTIONS),
-           "shud_ode.h": ("shud_ode_", abi.ODE_FUNCTIONS)}
+           "shud_ode.h": ("shud_ode_", abi.ODE_FUNCTIONS), "shud_out.h": ("shud_(?:out|rhs)_", abi.OUT_FUNCTIONS)}
 LIB = os.path.join(ROOT, "shud-up_amd", "libshud_rhs.so")
 
 
@@ -42,7 +42,7 @@ def test_library_exports_every_symbol():
 
 
 def _c_sizeof(struct):
-    src = f'#include "shud_rhs.h"\n#include "shud_et.h"\n#include "shud_ode.h"\n#include <stdio.h>\nint main(){{printf("%zu\\n", sizeof({struct}));return 0;}}\n'
+    src = f'#include "shud_rhs.h"\n#include "shud_et.h"\n#include "shud_ode.h"\n#include "shud_out.h"\n#include <stdio.h>\nint main(){{printf("%zu\\n", sizeof({struct}));return 0;}}\n'
     exe = f"/tmp/sz_{struct}_{os.getpid()}"
     subprocess.run(["gcc", "-x", "c", "-", "-I", os.path.join(ROOT, "include"), "-o", exe], input=src.encode(),
                    check=True)
@@ -58,5 +58,5 @@ def test_struct_layouts_match_header():
                       ("ShudPartition", abi.ShudPartition), ("ShudEtMeshSoA", abi.ShudEtMeshSoA),
                       ("ShudEtParams", abi.ShudEtParams), ("ShudEtForcing", abi.ShudEtForcing),
                       ("ShudEtOut", abi.ShudEtOut), ("ShudOdeOptions", abi.ShudOdeOptions),
-                      ("ShudOdeStats", abi.ShudOdeStats)]:
+                      ("ShudOdeStats", abi.ShudOdeStats), ("ShudPrintSpec", abi.ShudPrintSpec)]:
         assert C.sizeof(cls) == _c_sizeof(name), name

@@ -165,3 +165,27 @@ def test_device_leaf_kat_vs_oracle(name):
     else:
         ok = _same(got, want) & (np.signbit(got) == np.signbit(want))
     assert ok.all(), f"{name}: {(~ok).sum()} of {x.shape[0]} differ, first row {x[np.argmax(~ok)]}"
+
+
+@pytest.mark.gpu
+def test_pow_pos_bit_identical():
+    """pow_pos (shud_physics.h: OCML's pow core without its special-case selects) returns the same bits as the
+    device's full pow on satKfun's domain — bases in (0, 1] (satn in (ZERO, 0.99], 1 - satn^ex1), exponents
+    n/(n-1) and (n-1)/n of Beta > 1 — and on a wider positive grid."""
+    lib = C.CDLL(os.path.join(PKG_DIR, "libshud_kat.so"))
+    lib.shud_kat_pow.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_void_p]
+    rng = np.random.default_rng(7)
+    n = 1 << 20
+    beta = np.concatenate([1.0 + rng.uniform(1e-6, 4.0, n // 2), 1.0 + 10 ** rng.uniform(-12, 3, n // 2)])
+    x = np.concatenate([rng.uniform(1e-10, 0.99, n // 4), 10 ** rng.uniform(-10, 0, n // 4),
+                        1.0 - 10 ** rng.uniform(-17, -0.01, n // 4), 10 ** rng.uniform(-300, 300, n // 4)])
+    y = np.where(rng.random(n) < 0.5, beta / (beta - 1.0), (beta - 1.0) / beta)
+    edge_x = np.array([1.0, 0.99, 1e-10, 0.5, np.nextafter(1.0, 0.0), 5e-324, 2.2250738585072014e-308])
+    edge_y = np.array([3.0, 1.0, 0.5, 2.0, 1e6, 1.0, 1.0])
+    xy = np.ascontiguousarray(np.stack([np.concatenate([x, edge_x]), np.concatenate([y, edge_y])], 1))
+    m = xy.shape[0]
+    full, fast = np.zeros(m), np.zeros(m)
+    assert lib.shud_kat_pow(0, xy.ctypes.data, m, full.ctypes.data) == 0
+    assert lib.shud_kat_pow(1, xy.ctypes.data, m, fast.ctypes.data) == 0
+    same = full.view(np.uint64) == fast.view(np.uint64)
+    assert same.all(), f"{(~same).sum()} differ, first (x, y) = {xy[np.argmax(~same)]}"
