@@ -6,10 +6,15 @@
 
 namespace shud {
 
+// counted warnings spread over kWarnSlots counters, one 128-B L2 line each (slot = workgroup index mod
+// kWarnSlots): inputs that warn on every element then cost parallel atomics on 64 lines, not a serial
+// chain on one address; the host sums the slots when it reads the error word
+constexpr int kWarnSlots = 64, kWarnStride = 16;
 struct DevErr {                      // per-handle device error word (ShudErr on the host)
     uint32_t flags;
     int32_t first_index[8];          // slot = log2(bit); INT32_MAX = none
-    unsigned long long n_warn;
+    unsigned long long n_warn;       // host side: sum of the slots
+    unsigned long long *warn;        // [kWarnSlots * kWarnStride] device counters
 };
 
 struct DevMesh {

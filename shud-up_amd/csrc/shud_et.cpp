@@ -208,8 +208,7 @@ extern "C" int shud_et_step(shud_rhs_t h, const ShudEtForcing *f) {
     h->fu_unit[0] = h->fu_unit[1] = !p.cryosphere;
     h->have_last = false;                 // step inputs changed: no diagnostic replay of the last RHS
     // the reference exits from tReadForcing (myexit(10)); report it like the RHS errors
-    HIP_TRY(hipMemcpyAsync(h->h_err, h->d_err, sizeof(DevErr), hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(hipStreamSynchronize(h->stream));
+    if (int rc = shud_read_err(h)) return rc;
     if (h->h_err->flags & (SHUD_EF_ET_RA | SHUD_EF_ET_PT_NAN))
         return shud_fail(SHUD_ERR_PHYSICS, "ET prelude error flags 0x%x", h->h_err->flags);
     return SHUD_OK;

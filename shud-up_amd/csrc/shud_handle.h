@@ -78,6 +78,8 @@ struct shud_rhs {
 
     DevErr *d_err = nullptr;
     DevErr *h_err = nullptr;             // pinned
+    unsigned long long *d_warn = nullptr;   // DevErr::warn slots
+    unsigned long long *h_warn = nullptr;   // pinned
 
     // partition / halo
     bool partitioned = false;
@@ -118,5 +120,6 @@ struct shud_rhs {
 };
 
 int shud_reset_err(shud_rhs *h);
+int shud_read_err(shud_rhs *h);          // h_err = the device error word (warning slots summed); synchronises
 int shud_diag_replay(shud_rhs *h);       // shud_rhs.cpp: last eval again with diagnostic stores (device only)
 void shud_et_free(shud_rhs *h);          // shud_et.cpp

@@ -82,6 +82,7 @@ struct shud_ode {
     double tau[kQMax + 2]{}, tq[6]{}, l[kQMax + 1]{};
     double rl1 = 0, gamma = 0, gammap = 0, gamrat = 1, crate = 1, delp = 0, acnrm = 0, saved_tq5 = 0;
     double tstop = 0, tretlast = 0, tolsf = 1, etaq = 0, etaqm1 = 0, etaqp1 = 0, nrmfac = 1;
+    bool acor_zero = false;
     int tstopset = 0, q = 1, qprime = 1, next_q = 1, qwait = 2, L = 2, qu = 0, indx_acor = 5;
     int convfail = 0, jcur = 0, jbad = 0, curiter = 0, initialized = 0;
     int64_t nst = 0, nscon = 0, nstlp = 0, nfe = 0, nfeDQ = 0, nni = 0, nnf = 0, ncfn = 0, netf = 0, nsetups = 0;
@@ -376,10 +377,15 @@ struct shud_ode {
 
     // ---- cvNls with the Newton SUNNonlinearSolver ----
     int nls_residual() {                                             // cvNlsResidual (+ -delta, + bnorm)
-        vsum(n, Z(0), acor, y, s);
+        // acor_zero: cvNls has just set ycor = 0; the zero fill is fused into the y = zn[0] + ycor pass and
+        // the residual reads no ycor (identical operands, one fewer pass over HBM)
+        const bool az = acor_zero;
+        acor_zero = false;
+        if (az) vsum_zero(n, Z(0), acor, y, s);
+        else vsum(n, Z(0), acor, y, s);
         if (rhs(tn, y, ftemp) != 0) return SHUD_ODE_RHSFUNC_FAIL;
         nfe++;
-        residual(n, Z(1), acor, ftemp, rl1, -gamma, ewt, delta, red, s);
+        residual(n, Z(1), az ? nullptr : acor, ftemp, rl1, -gamma, ewt, delta, red, s);
         finalize(red, 1, 0u, d_ds, S_RES, s);
         if (!fetch()) return SHUD_ODE_RHSFUNC_FAIL;
         return 0;
@@ -400,7 +406,7 @@ struct shud_ode {
         convfail = (nflag == FIRST_CALL || nflag == PREV_ERR_FAIL) ? CV_NO_FAILURES : CV_FAIL_OTHER;
         int callSetup = (nflag == PREV_CONV_FAIL) || (nflag == PREV_ERR_FAIL) || (nst == 0) ||
                         (nst >= nstlp + MSBP) || (std::fabs(gamrat - 1.0) > DGMAX);
-        zero(n, acor, s);
+        acor_zero = true;                              // N_VConst(0, ycor), fused (nls_residual)
         int jb = 0, rv = 0;
         for (;;) {
             rv = nls_residual();
@@ -431,7 +437,7 @@ struct shud_ode {
                 nnf++;
                 callSetup = 1;
                 jb = 1;
-                zero(n, acor, s);
+                acor_zero = true;                              // N_VConst(0, ycor), fused (nls_residual)
                 continue;
             }
             break;

@@ -55,6 +55,7 @@ void predict(int64_t n, double *zn, int q, hipStream_t s);
 void restore(int64_t n, double *zn, int q, hipStream_t s);
 void rescale(int64_t n, double *zn, int q, const Coefs &c, hipStream_t s);
 void vsum(int64_t n, const double *x, const double *y, double *z, hipStream_t s);
+void vsum_zero(int64_t n, const double *x, double *ycor, double *z, hipStream_t s);   // ycor = 0; z = x + 0
 void copy(int64_t n, const double *x, double *z, hipStream_t s);
 void scale_to(int64_t n, double c, const double *x, double *z, hipStream_t s);
 void zero(int64_t n, double *z, hipStream_t s);

@@ -136,6 +136,20 @@ __global__ void __launch_bounds__(kThreads) k_vsum(int64_t n, const double *__re
 void vsum(int64_t n, const double *x, const double *y, double *z, hipStream_t s) {
     k_vsum<<<grid_blocks(n), kThreads, 0, s>>>(n, x, y, z);
 }
+// cvNls's N_VConst(0, ycor) fused into cvNlsResidual's N_VLinearSum(1, zn[0], 1, ycor, y): ycor = 0 and
+// z = x + 0.0 (the same add as k_vsum with a zero operand, so -0.0 becomes +0.0 exactly as there).  24 B/entry
+// instead of a 8 B/entry fill plus 24 B/entry.
+__global__ void __launch_bounds__(kThreads) k_vsum_zero(int64_t n, const double *__restrict__ x,
+                                                        double *__restrict__ ycor, double *__restrict__ z) {
+    GRID_LOOP(i, n) {
+        const double zero = 0.0;
+        ycor[i] = zero;
+        z[i] = x[i] + zero;
+    }
+}
+void vsum_zero(int64_t n, const double *x, double *ycor, double *z, hipStream_t s) {
+    k_vsum_zero<<<grid_blocks(n), kThreads, 0, s>>>(n, x, ycor, z);
+}
 
 __global__ void __launch_bounds__(kThreads) k_scale_to(int64_t n, double c, const double *x, double *z) {
     GRID_LOOP(i, n) z[i] = c * x[i];
@@ -169,7 +183,7 @@ __global__ void __launch_bounds__(kThreads) k_residual(int64_t n, const double *
                                                        double *__restrict__ delta, Red r) {
     double v[1] = {0.0};
     GRID_LOOP(i, n) {
-        const double r1 = rl1 * zn1[i] + ycor[i];
+        const double r1 = rl1 * zn1[i] + (ycor ? ycor[i] : 0.0);     // ycor == nullptr: ycor is all +0.0
         const double r2 = r1 + ngamma * ftemp[i];
         const double d = -r2;
         delta[i] = d;

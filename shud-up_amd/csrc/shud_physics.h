@@ -213,16 +213,21 @@ __device__ __forceinline__ double da_to_dy(double dA, double w_top, double s) {
 
 
 // record an error / warning, aggregated per wave: one lane (the lowest flagged lane = lowest element index
-// of the wave, since lanes map to consecutive indices) does the atomics for the whole wave, so inputs that
-// flag millions of elements cost one atomic per wave instead of serialising on one address.  Must be
-// reached by every active lane (it is a __ballot).
+// of the wave, since lanes map to consecutive indices) does the atomics for the whole wave.  flags only gain
+// bits and first_index only decreases, so a plain load that already shows the bit / a smaller index proves
+// the atomic would change nothing (a stale load can only cost a redundant atomic): inputs that flag every
+// element then issue ~no atomics on the shared word, and the warning count goes to one of kWarnSlots
+// lines.  Must be reached by every active lane (it is a __ballot).
 __device__ __forceinline__ void report_w(DevErr *e, bool c, uint32_t bit, int slot, int idx, bool count = false) {
     const unsigned long long mask = __ballot(c);
     if (mask == 0ULL) return;
     if ((int)__lane_id() == __ffsll((long long)mask) - 1) {
-        atomicOr(&e->flags, bit);
-        atomicMin(&e->first_index[slot], idx);
-        if (count) atomicAdd(&e->n_warn, (unsigned long long)__popcll(mask));
+        if (!(__atomic_load_n(&e->flags, __ATOMIC_RELAXED) & bit)) atomicOr(&e->flags, bit);
+        if (__atomic_load_n(&e->first_index[slot], __ATOMIC_RELAXED) > idx) atomicMin(&e->first_index[slot], idx);
+        if (count) {
+            unsigned long long *w = __atomic_load_n(&e->warn, __ATOMIC_RELAXED);
+            atomicAdd(w + (blockIdx.x & (kWarnSlots - 1)) * kWarnStride, (unsigned long long)__popcll(mask));
+        }
     }
 }
 

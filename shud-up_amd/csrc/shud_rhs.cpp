@@ -47,6 +47,8 @@ int shud_reset_err(shud_rhs *h) {
     z.flags = 0;
     for (int k = 0; k < 8; k++) z.first_index[k] = INT_MAX;
     z.n_warn = 0;
+    z.warn = h->d_warn;
+    HIP_TRY(hipMemsetAsync(h->d_warn, 0, kWarnSlots * kWarnStride * sizeof(unsigned long long), h->stream));
     HIP_TRY(hipMemcpyAsync(h->d_err, &z, sizeof(DevErr), hipMemcpyHostToDevice, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     return 0;
@@ -296,8 +298,11 @@ static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, cons
     if ((rc = build_packed(h, m, p, eflags, seg_off, up_off, up_idx))) return rc;
     if (h->lakeon && (rc = build_lakes(h, m))) return rc;
     if ((rc = h->dalloc(&h->d_err, 1))) return rc;
+    if ((rc = h->dalloc(&h->d_warn, (size_t)kWarnSlots * kWarnStride))) return rc;
     d.err = h->d_err;
     HIP_TRY(hipHostMalloc((void **)&h->h_err, sizeof(DevErr), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void **)&h->h_warn, kWarnSlots * kWarnStride * sizeof(unsigned long long),
+                          hipHostMallocDefault));
     if ((rc = shud_reset_err(h))) return rc;
     const size_t ny = 3 * (size_t)h->n_own + h->n_own_riv + h->NL;
     if ((rc = h->dalloc(&h->d_y, ny))) return rc;
@@ -593,6 +598,7 @@ static void destroy_handle(shud_rhs *h) {
     if (h->s_comm) (void)hipStreamDestroy(h->s_comm);
     for (void *p : h->allocs) (void)hipFree(p);
     if (h->h_err) (void)hipHostFree(h->h_err);
+    if (h->h_warn) (void)hipHostFree(h->h_warn);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -736,11 +742,19 @@ static void flip(shud_rhs *h) {
     else if (h->mode == SHUD_MODE_SERIAL) h->cur_e ^= 1;
 }
 
-static int read_err(shud_rhs *h) {
+int shud_read_err(shud_rhs *h) {
     HIP_TRY(hipMemcpyAsync(h->h_err, h->d_err, sizeof(DevErr), hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
+    h->h_err->n_warn = 0;
+    if (h->h_err->flags & SHUD_EF_AET_WARN) {          // the only counted report
+        HIP_TRY(hipMemcpyAsync(h->h_warn, h->d_warn, kWarnSlots * kWarnStride * sizeof(unsigned long long),
+                               hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        for (int k = 0; k < kWarnSlots; k++) h->h_err->n_warn += h->h_warn[k * kWarnStride];
+    }
     return 0;
 }
+static int read_err(shud_rhs *h) { return shud_read_err(h); }
 
 static const uint32_t kFatal = SHUD_EF_NAN_QELE | SHUD_EF_EFFKH | SHUD_EF_ET_NEG | SHUD_EF_ET_NAN;
 
