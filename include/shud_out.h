@@ -54,6 +54,12 @@ enum {
     SHUD_ARR_Q_PRCP,             /* qElePrep                                     NE  */
     SHUD_ARR_Q_NET_PRCP,         /* qEleNetPrep                                  NE  */
     SHUD_ARR_Q_ETP,              /* qEleETP                                      NE  */
+    /* ET-step prelude state (shud_et_attach'ed handles; NULL otherwise) */
+    SHUD_ARR_Y_ELE_IS,           /* yEleIS (interception storage)                NE  */
+    SHUD_ARR_Y_ELE_SNOW,         /* yEleSnow                                     NE  */
+    SHUD_ARR_RN_H,               /* ele_rn_h_wm2: forcing shortwave (MD_ET.cpp:201) NE */
+    SHUD_ARR_RN_T,               /* ele_rn_t_wm2: terrain-corrected shortwave    NE  */
+    SHUD_ARR_RN_FACTOR,          /* ele_rn_factor: TSR factor                    NE  */
     SHUD_ARR_COUNT
 };
 
@@ -62,6 +68,9 @@ int shud_rhs_summary(shud_rhs_t h, const double *d_y);
 /* replays the last RHS evaluation with diagnostic stores into the device arrays (no host copy; carried
  * state unchanged): what the reference's flux arrays hold after CVODE's last f() call */
 int shud_rhs_refresh_diagnostics(shud_rhs_t h);
+/* allocates every array above (zero-filled) without evaluating anything, so print controls can be registered
+ * before the first RHS call (the serial RHS is stateful: an extra evaluation would change the trajectory) */
+int shud_rhs_prepare_outputs(shud_rhs_t h);
 /* device pointer of one of the arrays above (NULL if unknown / not yet materialised) and its length */
 const double *shud_rhs_device_array(shud_rhs_t h, int which, int64_t *n);
 

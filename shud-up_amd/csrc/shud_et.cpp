@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "shud_et.h"
+#include "shud_out.h"
 #include "shud_et_dev.h"
 #include "shud_handle.h"
 
@@ -79,7 +80,7 @@ extern "C" int shud_et_attach(shud_rhs_t h, const ShudEtMeshSoA *m, const ShudEt
     e.iforc = iforc; e.ilc = ilc; e.imf = imf; e.ilake = ilake;
     e.z_surf = dz; e.albedo = dalb; e.fixp = dfp; e.windh = dwh; e.vegf = dvf; e.nx = dnx; e.ny = dny; e.nz = dnz;
     double **state[] = {&e.y_is, &e.y_snow, &e.tsr_factor, &e.tacc_surf, &e.tacc_sub, &e.acc_surf, &e.acc_sub,
-                        &e.t_prcp, &e.t_temp, &e.t_mf, &e.t_rn, &e.t_wind, &e.t_rh, &e.rn_factor};
+                        &e.t_prcp, &e.t_temp, &e.t_mf, &e.t_rn, &e.t_wind, &e.t_rh, &e.rn_factor, &e.rn_h, &e.rn_t};
     for (double **q : state)
         if ((rc = h->upload(q, (const double *)nullptr, NE))) return rc;   // zero: ACC starts at 0 (see DESIGN)
     if (p->cryosphere) {
@@ -230,4 +231,17 @@ extern "C" int shud_et_get(shud_rhs_t h, ShudEtOut *o) {
     for (auto &x : m)
         if (x.dst) HIP_TRY(hipMemcpy(x.dst, x.src, nb, hipMemcpyDeviceToHost));
     return SHUD_OK;
+}
+
+const double *shud_et_array(shud_rhs *h, int which) {
+    if (!h || !h->et) return nullptr;
+    const DevEt &e = h->et->e;
+    switch (which) {
+        case SHUD_ARR_Y_ELE_IS: return e.y_is;
+        case SHUD_ARR_Y_ELE_SNOW: return e.y_snow;
+        case SHUD_ARR_RN_H: return e.rn_h;
+        case SHUD_ARR_RN_T: return e.rn_t;
+        case SHUD_ARR_RN_FACTOR: return e.rn_factor;
+        default: return nullptr;
+    }
 }

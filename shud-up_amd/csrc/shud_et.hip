@@ -206,6 +206,7 @@ __global__ void __launch_bounds__(256) shud_et_kernel(DevEt e, EtStepDev s, DevE
     // ---- outputs: diagnostics + the RHS step inputs ----
     e.t_prcp[i] = prcp; e.t_temp[i] = temp; e.t_lai[i] = lai; e.t_mf[i] = mf; e.t_rn[i] = rn;
     e.t_wind[i] = wind; e.t_rh[i] = rh; e.rn_factor[i] = factor;
+    e.rn_h[i] = dswrf_h; e.rn_t[i] = dswrf_t;
     e.q_prep[i] = prcp; e.q_pet[i] = qpet; e.q_ptr[i] = qptr; e.q_etp[i] = etp; e.q_netp[i] = netp;
     e.q_eic[i] = eic; e.fu_surf[i] = fu_surf; e.fu_sub[i] = fu_sub;
     if (s.packed) {                                   // the element kernel's records (shud_dev.h DevPacked)

@@ -14,6 +14,7 @@ struct DevEt {                       // per element: statics, carried state, out
     double *ring_surf, *ring_sub;                             // cryosphere day-mean queues [cap][ne]
     double *tacc_surf, *tacc_sub, *acc_surf, *acc_sub;        // T_AccDay, ACC per element
     double *t_prcp, *t_temp, *t_lai, *t_mf, *t_rn, *t_wind, *t_rh, *rn_factor;
+    double *rn_h, *rn_t;                                      // ele_rn_h_wm2 / ele_rn_t_wm2 (MD_ET.cpp:201-202)
     double *q_prep, *q_pet, *q_ptr, *q_etp, *q_netp, *q_eic, *fu_surf, *fu_sub;
 };
 

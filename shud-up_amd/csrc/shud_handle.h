@@ -122,4 +122,6 @@ struct shud_rhs {
 int shud_reset_err(shud_rhs *h);
 int shud_read_err(shud_rhs *h);          // h_err = the device error word (warning slots summed); synchronises
 int shud_diag_replay(shud_rhs *h);       // shud_rhs.cpp: last eval again with diagnostic stores (device only)
+int shud_ensure_diag(shud_rhs *h);       // shud_rhs.cpp: allocate the DevDiag arrays (zeros) once
 void shud_et_free(shud_rhs *h);          // shud_et.cpp
+const double *shud_et_array(shud_rhs *h, int which);   // shud_et.cpp: SHUD_ARR_Y_ELE_IS.. (NULL if not attached)

@@ -253,6 +253,21 @@ extern "C" int shud_out_destroy(shud_out_t o) {
 // ---------------------------------------------------------------------------------------------
 // device sources on the RHS handle
 // ---------------------------------------------------------------------------------------------
+extern "C" int shud_rhs_prepare_outputs(shud_rhs_t h) {
+    if (!h) return shud_fail(SHUD_ERR_ARG, "null argument");
+    HIP_TRY(hipSetDevice(h->device));
+    const size_t len[5] = {(size_t)h->n_own, (size_t)h->n_own, (size_t)h->n_own, (size_t)h->n_own_riv,
+                           (size_t)h->NL};
+    int rc;
+    for (int k = 0; k < 5; k++)
+        if (!h->d_sum[k] && (rc = h->upload(&h->d_sum[k], (const double *)nullptr, len[k]))) return rc;
+    if ((rc = shud_ensure_diag(h))) return rc;
+    if (!h->d_trans && ((rc = h->upload(&h->d_trans, (const double *)nullptr, h->NE)) ||
+                        (rc = h->upload(&h->d_evapo, (const double *)nullptr, h->NE))))
+        return rc;
+    return SHUD_OK;
+}
+
 extern "C" int shud_rhs_summary(shud_rhs_t h, const double *d_y) {
     if (!h || !d_y) return shud_fail(SHUD_ERR_ARG, "null argument");
     HIP_TRY(hipSetDevice(h->device));
@@ -316,6 +331,11 @@ extern "C" const double *shud_rhs_device_array(shud_rhs_t h, int which, int64_t 
         case SHUD_ARR_Q_PRCP: p = h->dm.prcp; len = ne; break;
         case SHUD_ARR_Q_NET_PRCP: p = h->dm.net_prep; len = ne; break;
         case SHUD_ARR_Q_ETP: p = h->dm.etp; len = ne; break;
+        case SHUD_ARR_Y_ELE_IS: p = shud_et_array(h, which); len = ne; break;
+        case SHUD_ARR_Y_ELE_SNOW: p = shud_et_array(h, which); len = ne; break;
+        case SHUD_ARR_RN_H: p = shud_et_array(h, which); len = ne; break;
+        case SHUD_ARR_RN_T: p = shud_et_array(h, which); len = ne; break;
+        case SHUD_ARR_RN_FACTOR: p = shud_et_array(h, which); len = ne; break;
         default: break;
     }
     if (n) *n = p ? len : 0;

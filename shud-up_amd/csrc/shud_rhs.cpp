@@ -887,7 +887,7 @@ extern "C" int shud_rhs_cvrhs(double t, const double *y, double *ydot, void *use
 // ---------------------------------------------------------------------------------------------
 // diagnostics (replay of the last call with DIAG kernels)
 // ---------------------------------------------------------------------------------------------
-static int ensure_diag(shud_rhs *h) {
+int shud_ensure_diag(shud_rhs *h) {
     if (h->have_diag) return 0;
     const size_t NE = h->NE, NR = h->NR;
     double **e1[] = {&h->dd.qele_surf_tot, &h->dd.qele_sub_tot, &h->dd.q_infil, &h->dd.q_exfil, &h->dd.q_recharge,
@@ -914,7 +914,7 @@ static int ensure_diag(shud_rhs *h) {
 int shud_diag_replay(shud_rhs *h) {
     if (!h->have_last) return shud_fail(SHUD_ERR_ARG, "no evaluation to report diagnostics for");
     HIP_TRY(hipSetDevice(h->device));
-    int rc = ensure_diag(h);
+    int rc = shud_ensure_diag(h);
     if (rc) return rc;
     launch_all(h, h->last_y, h->d_scratch_dy, h->last_cur, h->last_cur_e, true);
     HIP_TRY(hipGetLastError());

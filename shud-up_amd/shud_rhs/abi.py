@@ -213,7 +213,8 @@ ODE_FUNCTIONS = {
  SHUD_ARR_QELE_SURF_TOT, SHUD_ARR_QELE_SUB_TOT, SHUD_ARR_QELE_SURF, SHUD_ARR_QELE_SUB, SHUD_ARR_QE2R_SURF,
  SHUD_ARR_QE2R_SUB, SHUD_ARR_Q_INFIL, SHUD_ARR_Q_EXFIL, SHUD_ARR_Q_RECHARGE, SHUD_ARR_Q_ETA, SHUD_ARR_Q_E_IC,
  SHUD_ARR_Q_TRANS, SHUD_ARR_Q_EVAPO, SHUD_ARR_QRIV_DOWN, SHUD_ARR_QRIV_UP, SHUD_ARR_QRIV_SURF, SHUD_ARR_QRIV_SUB,
- SHUD_ARR_Q_PRCP, SHUD_ARR_Q_NET_PRCP, SHUD_ARR_Q_ETP, SHUD_ARR_COUNT) = range(26)
+ SHUD_ARR_Q_PRCP, SHUD_ARR_Q_NET_PRCP, SHUD_ARR_Q_ETP, SHUD_ARR_Y_ELE_IS, SHUD_ARR_Y_ELE_SNOW, SHUD_ARR_RN_H,
+ SHUD_ARR_RN_T, SHUD_ARR_RN_FACTOR, SHUD_ARR_COUNT) = range(31)
 
 
 class ShudPrintSpec(C.Structure):
@@ -226,6 +227,7 @@ class ShudPrintSpec(C.Structure):
 OUT_FUNCTIONS = {
     "shud_rhs_summary": (C.c_int, [_H, C.c_void_p]),
     "shud_rhs_refresh_diagnostics": (C.c_int, [_H]),
+    "shud_rhs_prepare_outputs": (C.c_int, [_H]),
     "shud_rhs_device_array": (C.c_void_p, [_H, C.c_int, C.POINTER(C.c_int64)]),
     "shud_out_create": (C.c_int, [C.c_int, C.c_void_p, C.POINTER(_H)]),
     "shud_out_add": (C.c_int, [_H, C.POINTER(ShudPrintSpec)]),

@@ -173,6 +173,10 @@ class RhsHandle:
         """the last RHS evaluation replayed with diagnostic stores into the device arrays (no host copy)"""
         _check(lib().shud_rhs_refresh_diagnostics(self.h), "refresh_diagnostics")
 
+    def prepare_outputs(self):
+        """allocate every device output array (zeros) without evaluating anything (shud_rhs_prepare_outputs)"""
+        _check(lib().shud_rhs_prepare_outputs(self.h), "prepare_outputs")
+
     def device_array(self, which):
         n = C.c_int64()
         p = lib().shud_rhs_device_array(self.h, int(which), C.byref(n))

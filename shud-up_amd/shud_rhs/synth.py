@@ -169,3 +169,142 @@ def synth_model(n_target, seed=12345, h=100.0, stem_every=12, reach_quads=3):
     m.seg_cwr = R["Cwr"][rt[seg_riv]]
     m.meta.update(prj=f"syn-{NE}", nqx=nqx, nqy=nqy, x=ext["x"], y=ext["y"], seed=seed)
     return m.finalize()
+
+
+# ---------------------------------------------------------------------------------------------------------
+# SHUD text-format project writer ("the synthetic-mesh generator at scale"): the same seeded
+# mesh / river tree as synth_model, written as the reference's input files so the C++ host (shud_gpu,
+# include/shud_host.h) and the Python readers (shudio) can load it like input/<prj>/.  Numbers are written
+# with 17 significant digits, so every value reads back bit for bit.
+# ---------------------------------------------------------------------------------------------------------
+def _fmt(v):
+    return f"{float(v):.17g}" if isinstance(v, (float, np.floating)) else str(int(v))
+
+
+def _write_table(f, header, rows, extra=""):
+    rows = list(rows)
+    ncol = len(header)
+    f.write(f"{len(rows)}\t{ncol}{extra}\n")
+    f.write("\t".join(header) + "\n")
+    for r in rows:
+        f.write("\t".join(_fmt(v) for v in r) + "\n")
+
+
+def synth_raw(n_target, seed=12345, h=100.0, stem_every=12, reach_quads=3):
+    """Raw (file-level) description of synth_model's mesh: nodes, triangles, neighbours, attribute rows,
+    reaches and segments, with the random draws in synth_model's order."""
+    m = synth_model(n_target, seed=seed, h=h, stem_every=stem_every, reach_quads=reach_quads)
+    rng = np.random.default_rng(seed)
+    soil, geol, lc, rtype, att_rows, cal = load_tables()
+    nqx, nqy = grid_dims(n_target)
+    nnx, nny = nqx + 1, nqy + 1
+    ii, jj = np.meshgrid(np.arange(nnx), np.arange(nny))
+    x = (ii * h + rng.uniform(-0.2 * h, 0.2 * h, ii.shape)).reshape(-1)
+    y = (jj * h + rng.uniform(-0.2 * h, 0.2 * h, jj.shape)).reshape(-1)
+    xbar = 0.5 * nqx * h
+    zmax = 1000.0 + 0.02 * y + 0.01 * np.abs(x - xbar) + 2.0 * np.sin(x / 700.0) * np.cos(y / 900.0)
+    qi, qj = np.meshgrid(np.arange(nqx), np.arange(nqy))
+    qi, qj = qi.reshape(-1), qj.reshape(-1)
+    A = qj * nnx + qi
+    B, Cn, D = A + 1, A + nnx + 1, A + nnx
+    ax, ay, bx, by, cx, cy, dx, dy = x[A], y[A], x[B], y[B], x[Cn], y[Cn], x[D], y[D]
+    adx, ady, bdx, bdy, cdx, cdy = ax - dx, ay - dy, bx - dx, by - dy, cx - dx, cy - dy
+    det = ((adx * adx + ady * ady) * (bdx * cdy - cdx * bdy) - (bdx * bdx + bdy * bdy) * (adx * cdy - cdx * ady)
+           + (cdx * cdx + cdy * cdy) * (adx * bdy - bdx * ady))
+    use_bd = det > 0
+    t0 = np.where(use_bd[:, None], np.stack([A, B, D], 1), np.stack([A, B, Cn], 1))
+    t1 = np.where(use_bd[:, None], np.stack([B, Cn, D], 1), np.stack([A, Cn, D], 1))
+    tri = np.empty((2 * qi.size, 3), dtype=np.int64)
+    tri[0::2] = t0
+    tri[1::2] = t1
+    pick = att_rows[rng.integers(0, att_rows.shape[0], tri.shape[0])]
+    return m, dict(x=x, y=y, zmax=zmax, aqd=np.full(x.size, 30.0), tri=tri, pick=pick, soil=soil, geol=geol,
+                   lc=lc, rtype=rtype, cal=cal)
+
+
+def write_project(outdir, prj, n_target, days=2.0, seed=12345, max_step=10.0, et_step=60.0, dt_out=60,
+                  forcing_dt_min=60.0, extra_para=None):
+    """Write input files <outdir>/<prj>.* for the synthetic mesh; returns the in-memory ShudModel."""
+    os.makedirs(outdir, exist_ok=True)
+    m, raw = synth_raw(n_target, seed=seed)
+    NE, NR, NS = m.num_ele, m.num_riv, m.num_seg
+    p = lambda ext: os.path.join(outdir, f"{prj}.{ext}")
+    nbr = m.nabr.reshape(3, NE)
+    with open(p("sp.mesh"), "w") as f:
+        _write_table(f, ["ID", "Node1", "Node2", "Node3", "Nabr1", "Nabr2", "Nabr3", "Zmax"],
+                     ([i + 1, *(raw["tri"][i] + 1), *(nbr[:, i] + 1), 0] for i in range(NE)))
+        _write_table(f, ["ID", "X", "Y", "AqDepth", "Elevation"],
+                     ([k + 1, raw["x"][k], raw["y"][k], raw["aqd"][k], raw["zmax"][k]] for k in range(raw["x"].size)))
+    pick = raw["pick"]
+    with open(p("sp.att"), "w") as f:
+        _write_table(f, ["INDEX", "SOIL", "GEOL", "LC", "FORC", "MF", "BC", "SS", "LAKE"],
+                     ([i + 1, pick[i, 0], pick[i, 1], pick[i, 2], 1, 1, 0, 0, 0] for i in range(NE)))
+    for ext, tab in (("para.soil", raw["soil"]), ("para.geol", raw["geol"]), ("para.lc", raw["lc"])):
+        with open(p(ext), "w") as f:
+            _write_table(f, [f"C{j}" for j in range(tab.shape[1])], ([int(r[0])] + [float(v) for v in r[1:]] for r in tab))
+    # reaches: type recovered from the parameter rows (riv_depth identifies the rtype row uniquely)
+    R = raw["rtype"]
+    cal = dict(raw["cal"])
+    depth_rows = R[:, 1] + cal.get("RIV_DPTH+", 1.0)
+    rt = np.array([int(np.nonzero(depth_rows == d)[0][0]) for d in m.riv["riv_depth"]])
+    down = m.riv_down.astype(np.int64)
+    with open(p("sp.riv"), "w") as f:
+        _write_table(f, ["Index", "Down", "Type", "Slope", "Length", "BC"],
+                     ([r + 1, down[r] + 1 if down[r] >= 0 else down[r], rt[r] + 1, float(m.riv["riv_bed_slope"][r]),
+                       float(m.riv["riv_length"][r]), 0] for r in range(NR)))
+        _write_table(f, ["Index", "Depth", "BankSlope", "Width", "Sinuosity", "Manning", "Cwr", "KsatH", "BedThick"],
+                     ([int(r[0])] + [float(v) for v in r[1:]] for r in R))
+    with open(p("sp.rivseg"), "w") as f:
+        _write_table(f, ["Index", "iRiv", "iEle", "Length"],
+                     ([s + 1, int(m.seg_riv[s]) + 1, int(m.seg_ele[s]) + 1, float(m.seg_length[s])] for s in range(NS)))
+    with open(p("cfg.calib"), "w") as f:
+        for k, v in sorted(cal.items()):
+            f.write(f"{k}\t{float(v):.17g}\n")
+    para = {"INIT_MODE": 3, "ABSTOL": 1e-4, "RELTOL": 1e-4, "INIT_SOLVER_STEP": 1, "MAX_SOLVER_STEP": max_step,
+            "LSM_STEP": et_step, "START": 0, "END": days, "TERRAIN_RADIATION": 1, "dt_ye_surf": dt_out,
+            "dt_ye_unsat": dt_out, "dt_ye_gw": dt_out, "dt_ye_snow": dt_out, "dt_qe_et": dt_out,
+            "dt_qe_prcp": dt_out, "dt_qe_infil": dt_out, "dt_qe_rech": dt_out, "dt_Qe_sub": dt_out,
+            "dt_Qe_surf": dt_out, "dt_yr_stage": dt_out, "dt_Qr_down": dt_out, "dt_Qr_up": dt_out,
+            "dt_Qr_surf": dt_out, "dt_Qr_sub": dt_out}
+    para.update(extra_para or {})
+    with open(p("cfg.para"), "w") as f:
+        for k, v in para.items():
+            f.write(f"{k}\t{v}\n")
+    # initial condition (INIT_MODE 3): wet surface in the valleys, unsat 20 %, gw 60 % of the aquifer
+    rng = np.random.default_rng(seed + 1)
+    aq = m.par["aquifer_depth"]
+    with open(p("cfg.ic"), "w") as f:
+        _write_table(f, ["Index", "Canopy", "Snow", "Surface", "Unsat", "GW"],
+                     ([i + 1, 0.0, 0.0, float(rng.uniform(0, 0.01)), float(0.2 * aq[i]), float(0.6 * aq[i])]
+                      for i in range(NE)))
+        _write_table(f, ["Index", "Stage"], ([r + 1, float(rng.uniform(0.1, 1.0))] for r in range(NR)))
+    # forcing: one station (ccw's coordinates), hourly prcp/temp/rh/wind/radiation, 20000101
+    nrow = int(np.ceil(days * 1440.0 / forcing_dt_min)) + 2
+    tday = np.arange(nrow) * forcing_dt_min / 1440.0
+    hour = (tday * 24.0) % 24.0
+    temp = 8.0 + 6.0 * np.sin((hour - 9.0) / 24.0 * 2 * np.pi) + rng.normal(0, 0.5, nrow)
+    prcp = np.where(rng.uniform(0, 1, nrow) < 0.15, rng.gamma(1.5, 8.0, nrow), 0.0)
+    rh = np.clip(0.6 + 0.2 * np.cos(hour / 24.0 * 2 * np.pi) + rng.normal(0, 0.05, nrow), 0.05, 1.0)
+    wind = np.abs(2.0 + rng.normal(0, 0.8, nrow))
+    rad = np.maximum(0.0, 800.0 * np.sin((hour - 6.0) / 12.0 * np.pi)) * (hour > 6) * (hour < 18)
+    with open(os.path.join(outdir, "forcing.csv"), "w") as f:
+        f.write(f"{nrow}\t6\t20000101\t20100101\n")
+        f.write("Time_Day\tAPCP\tTMP\tSPFH\tUGRD\tDSWRF\n")
+        for k in range(nrow):
+            f.write(f"{tday[k]:.17g}\t{prcp[k]:.17g}\t{temp[k]:.17g}\t{rh[k]:.17g}\t{wind[k]:.17g}\t{rad[k]:.17g}\n")
+    with open(p("tsd.forc"), "w") as f:
+        f.write("1 20000101\n\nID\tLon\tLat\tX\tY\tZ\tFilename\n")
+        f.write("1\t-122.71\t39.195\t0\t0\t-9999\tforcing.csv\n")
+    nlc = raw["lc"].shape[0]
+    months = int(days // 31) + 3
+    with open(p("tsd.lai"), "w") as f:
+        f.write(f"{months}\t{nlc + 1}\t20000101\n")
+        f.write("Time_Day\t" + "\t".join(f"X{j + 1}" for j in range(nlc)) + "\n")
+        for k in range(months):
+            f.write(f"{31 * k}\t" + "\t".join(f"{0.5 + 0.1 * j + 0.05 * k:.17g}" for j in range(nlc)) + "\n")
+    with open(p("tsd.mf"), "w") as f:
+        f.write(f"{months}\t2\t20000101\n")
+        f.write("Time_Day\tMF\n")
+        for k in range(months):
+            f.write(f"{31 * k}\t{0.0013 + 0.0001 * k:.17g}\n")
+    return m
