@@ -163,6 +163,8 @@ int main(int argc, char **argv) {
     }
 
     // ---- the time loop (shud.cpp:86-140) ----
+    shud_rhs_synchronize(h);
+    const auto loop0 = std::chrono::steady_clock::now();
     const bool et_sub = c.et_step > kZero && c.et_step + kZero < c.solver_step;
     double t = c.start_time, tnext = t;
     const long long nsteps = max_steps >= 0 && max_steps < c.num_steps ? max_steps : c.num_steps;
@@ -209,15 +211,23 @@ int main(int argc, char **argv) {
         }
         if (!quiet && c.verbose) printf("step %lld  t = %.3f min\n", i + 1, t);
     }
+    shud_rhs_synchronize(h);
+    const double loop_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - loop0).count();
     shud_out_destroy(out);
     ShudOdeStats st;
     shud_ode_get_stats(ode, &st);
     const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - wall0).count();
     if (!quiet)
         printf("* \t t = %.3f min  steps %lld  RHS %lld  Newton %lld  Krylov %lld  err-test fails %lld  "
-               "%d outputs  wall %.2f s\n",
+               "%d outputs  wall %.2f s (time loop %.2f s)\n",
                t, (long long)st.nst, (long long)(st.nfe + st.nfe_ls), (long long)st.nni, (long long)st.nli,
-               (long long)st.netf, nprint, wall);
+               (long long)st.netf, nprint, wall, loop_s);
+    // one machine-readable line (tools/e2e.sh)
+    printf("{\"shud_gpu\": {\"num_ele\": %d, \"t_end_min\": %.6f, \"solver_steps\": %lld, \"cvode_steps\": %lld, "
+           "\"rhs_evals\": %lld, \"newton_iters\": %lld, \"krylov_iters\": %lld, \"outputs\": %d, "
+           "\"wall_s\": %.4f, \"loop_s\": %.4f, \"exit\": %d}}\n",
+           mesh.num_ele, t, nsteps, (long long)st.nst, (long long)(st.nfe + st.nfe_ls), (long long)st.nni,
+           (long long)st.nli, nprint, wall, loop_s, rc);
     shud_ode_destroy(ode);
     shud_rhs_device_free(h, d_y);
     shud_rhs_destroy(h);

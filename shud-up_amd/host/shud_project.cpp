@@ -369,6 +369,10 @@ int load(Project &p, const char *indir, const char *prj, const char *cwd, double
         p.iss[i] = (int32_t)att.at(i, 7);
         p.ilake[i] = (int32_t)att.at(i, 8);
     }
+    for (int i = 0; i < NE; i++)
+        if (p.ibc[i] != 0)
+            return fail(&p, "element %d: iBC = %d needs the .tsd.ebc1/.tsd.ebc2 tables, which this host does not read",
+                        i + 1, p.ibc[i]);
     // segments -> RivID (MD_initialize.cpp:188-191), rmSinks (Model_Data.cpp:238-266): one pass in element
     // order, a raised element is seen raised by the later ones; then InitElement again
     std::vector<int> riv_id(NE, 0);
@@ -426,6 +430,9 @@ int load(Project &p, const char *indir, const char *prj, const char *cwd, double
         if (rt[r] < 0 || rt[r] >= nrt) return fail(&p, "river reach %d: type out of range", r + 1);
         p.riv_down[r] = down > 0 ? down - 1 : down;
         p.riv_bc[r] = (int32_t)riv.at(r, 5);
+        if (p.riv_bc[r] != 0)
+            return fail(&p, "river reach %d: BC = %d needs the .tsd.rbc1/.tsd.rbc2 tables, which this host does not read",
+                        r + 1, p.riv_bc[r]);
         p.riv_length[r] = riv.at(r, 4);
         p.riv_slope[r] = rmax(kMinRivSlope, riv.at(r, 3));
         rrough[r] = R_rough[rt[r]];
