@@ -55,6 +55,8 @@ typedef struct {
     int32_t column;                      /* InitIJ column (QeleSurf/QeleSub j) or -1                   */
     int32_t n_all;                       /* NumEle / NumRiv / NumLake                                  */
     int32_t interval, iflux;             /* Interval [min], 1 = flux (tau 1440)                        */
+    const int32_t *flag_io;              /* io_ele / io_riv / io_lake of <prj>.cfg.output (read_cfgout,
+                                            MD_readin.cpp:25-104); NULL = every column                   */
 } ShudOutputDecl;
 
 /* reads <indir>/<prj>.* and runs the reference's initialisation; `cwd` resolves the forcing csv paths
@@ -80,6 +82,12 @@ int shud_project_outputs(shud_project_t p, const char *outdir, ShudOutputDecl *d
  * bucket decision with the solar samples of a new forcing interval (MD_ET.cpp:60-136).  Errors as the
  * reference's movePointer (missing forcing data -> message, code ERRFileIO). */
 int shud_project_forcing(shud_project_t p, double t, double tout, ShudEtForcing *f);
+
+/* Boundary-condition rows at the current ET step (after shud_project_forcing): the rows of <prj>.tsd.ebc1 /
+ * .ebc2 / .rbc1 / .rbc2 that f_update reads through getX (MD_update.cpp:114-125, 145-160), as the ele_ybc /
+ * ele_qbc / riv_ybc / riv_qbc fields (n_* = data columns) of `in`; the other fields are left untouched.
+ * Returns 1 when the model has boundary conditions (pass `in` to shud_rhs_set_step_inputs), 0 otherwise. */
+int shud_project_bc_rows(shud_project_t p, ShudStepInputs *in);
 
 /* solarPosition(t_min, lat, lon, Time, tz) (SolarRadiation.cpp:92-176) with the project's ForcStartTime as
  * the base date: out[0..4] = cosZ, zenith, azimuth, declination, hourAngle (KAT tests) */

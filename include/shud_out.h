@@ -60,6 +60,14 @@ enum {
     SHUD_ARR_RN_H,               /* ele_rn_h_wm2: forcing shortwave (MD_ET.cpp:201) NE */
     SHUD_ARR_RN_T,               /* ele_rn_t_wm2: terrain-corrected shortwave    NE  */
     SHUD_ARR_RN_FACTOR,          /* ele_rn_factor: TSR factor                    NE  */
+    /* lake fluxes of the last RHS evaluation (lake models; MD_initialize.cpp:331-342 order) */
+    SHUD_ARR_LAKE_TOPAREA,       /* y2LakeArea                                   NL  */
+    SHUD_ARR_Q_LAKE_EVAP,        /* qLakeEvap                                    NL  */
+    SHUD_ARR_Q_LAKE_PRCP,        /* qLakePrcp                                    NL  */
+    SHUD_ARR_Q_LAKE_RIVIN,       /* QLakeRivIn                                   NL  */
+    SHUD_ARR_Q_LAKE_RIVOUT,      /* QLakeRivOut: zeroed by f_update, never assigned (MD_update.cpp:184) NL */
+    SHUD_ARR_Q_LAKE_SURF,        /* QLakeSurf                                    NL  */
+    SHUD_ARR_Q_LAKE_SUB,         /* QLakeSub                                     NL  */
     SHUD_ARR_COUNT
 };
 

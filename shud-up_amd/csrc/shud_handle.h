@@ -75,6 +75,7 @@ struct shud_rhs {
     // output path (shud_out.h): Model_Data::summary arrays and the derived ET sums, allocated on first use
     double *d_sum[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};   // yEleSurf/Unsat/GW, yRivStg, yLakeStg
     double *d_trans = nullptr, *d_evapo = nullptr;                      // qEleTrans, qEleEvapo
+    double *d_zero_lake = nullptr;                                      // QLakeRivOut (always 0)
 
     DevErr *d_err = nullptr;
     DevErr *h_err = nullptr;             // pinned

@@ -262,6 +262,7 @@ extern "C" int shud_rhs_prepare_outputs(shud_rhs_t h) {
     for (int k = 0; k < 5; k++)
         if (!h->d_sum[k] && (rc = h->upload(&h->d_sum[k], (const double *)nullptr, len[k]))) return rc;
     if ((rc = shud_ensure_diag(h))) return rc;
+    if (!h->d_zero_lake && (rc = h->upload(&h->d_zero_lake, (const double *)nullptr, std::max(h->NL, 1)))) return rc;
     if (!h->d_trans && ((rc = h->upload(&h->d_trans, (const double *)nullptr, h->NE)) ||
                         (rc = h->upload(&h->d_evapo, (const double *)nullptr, h->NE))))
         return rc;
@@ -336,6 +337,13 @@ extern "C" const double *shud_rhs_device_array(shud_rhs_t h, int which, int64_t 
         case SHUD_ARR_RN_H: p = shud_et_array(h, which); len = ne; break;
         case SHUD_ARR_RN_T: p = shud_et_array(h, which); len = ne; break;
         case SHUD_ARR_RN_FACTOR: p = shud_et_array(h, which); len = ne; break;
+        case SHUD_ARR_LAKE_TOPAREA: p = nl ? d.lake_toparea : nullptr; len = nl; break;
+        case SHUD_ARR_Q_LAKE_EVAP: p = nl ? d.q_lake_evap : nullptr; len = nl; break;
+        case SHUD_ARR_Q_LAKE_PRCP: p = nl ? d.q_lake_prcp : nullptr; len = nl; break;
+        case SHUD_ARR_Q_LAKE_RIVIN: p = nl ? d.q_lake_rivin : nullptr; len = nl; break;
+        case SHUD_ARR_Q_LAKE_RIVOUT: p = nl ? h->d_zero_lake : nullptr; len = nl; break;
+        case SHUD_ARR_Q_LAKE_SURF: p = nl ? d.q_lake_surf : nullptr; len = nl; break;
+        case SHUD_ARR_Q_LAKE_SUB: p = nl ? d.q_lake_sub : nullptr; len = nl; break;
         default: break;
     }
     if (n) *n = p ? len : 0;

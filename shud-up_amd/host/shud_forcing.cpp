@@ -8,6 +8,7 @@
 #include <strings.h>
 #include <sys/stat.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <fstream>
@@ -17,7 +18,7 @@
 
 namespace shudhost {
 
-static constexpr int kMaxLen = 1024;
+static constexpr int kMaxLen = 2048;             // MAXLEN (Macros.hpp:30)
 static constexpr int kNforc = 5;                  // Nforc (Macros.hpp:37): prcp, temp, rh, wind, rn
 
 static bool exists(const std::string &f) {
@@ -316,6 +317,38 @@ int read_forcing(Project &p, const char *cwd) {
     return 0;
 }
 
+int read_series_file(Project &p, Series &s) {
+    int rc = read_dims(p, s);
+    return rc ? rc : read_series(p, s);
+}
+int move_series(Project &p, Series &s, double t) { return move_pointer(p, s, t); }
+
+// read_bcEle1/2, read_bcRiv1/2 (MD_readin.cpp:959-982) when the mesh references them (ieBC1/2, irBC1/2)
+int read_bc(Project &p) {
+    static const char *ext[4] = {"tsd.ebc1", "tsd.ebc2", "tsd.rbc1", "tsd.rbc2"};
+    int maxc[4] = {0, 0, 0, 0};
+    for (int i = 0; i < p.NE; i++) {
+        if (p.ibc[i] > 0) maxc[0] = std::max(maxc[0], p.ibc[i]);
+        if (p.ibc[i] < 0) maxc[1] = std::max(maxc[1], -p.ibc[i]);
+    }
+    for (int r = 0; r < p.NR; r++) {
+        if (p.riv_bc[r] > 0) maxc[2] = std::max(maxc[2], p.riv_bc[r]);
+        if (p.riv_bc[r] < 0) maxc[3] = std::max(maxc[3], -p.riv_bc[r]);
+    }
+    for (int k = 0; k < 4; k++) {
+        if (!maxc[k]) continue;
+        p.bc[k].fn = p.indir + "/" + p.prj + "." + ext[k];
+        if (int rc = read_series_file(p, p.bc[k])) return rc;
+        p.have_bc[k] = true;
+        // getX(t, col) reads ts[iNow][col] unchecked: columns past the table read 0 here (warning)
+        p.bc_w[k] = std::max(p.bc[k].ncol, maxc[k] + 1);
+        if (p.bc_w[k] > p.bc[k].ncol)
+            fprintf(stderr, "WARNING: %s has %d columns but column %d is referenced; those read 0 here\n",
+                    p.bc[k].fn.c_str(), p.bc[k].ncol, maxc[k]);
+    }
+    return 0;
+}
+
 // One ET step: updateAllTimeSeries(t) (MD_update.cpp:3-40) and the shared part of tReadForcing (MD_ET.cpp:21-136)
 int step_forcing(Project &p, double t, double tout, ShudEtForcing *f) {
     int rc;
@@ -323,6 +356,8 @@ int step_forcing(Project &p, double t, double tout, ShudEtForcing *f) {
         if ((rc = move_pointer(p, s, t))) return rc;
     if (p.NumLC > 0 && (rc = move_pointer(p, p.lai, t))) return rc;
     if (p.mf.ncol > 0 && (rc = move_pointer(p, p.mf, t))) return rc;
+    for (int k = 0; k < 4; k++)                                        // tsd_eyBC .. tsd_rqBC (MD_update.cpp:25-40)
+        if (p.have_bc[k] && (rc = move_pointer(p, p.bc[k], t))) return rc;
     const int ns = (int)p.wx.size();
     p.st_rows.resize((size_t)ns * 6);
     p.st_z.resize(ns);

@@ -152,7 +152,7 @@ int main(int argc, char **argv) {
             return 1;
         }
         if (d.column >= 0) src += (size_t)d.column * mesh.num_ele;
-        ShudPrintSpec ps = {d.basename, src, d.n_all, nullptr, d.interval, d.iflux, (int64_t)c.forc_start_time,
+        ShudPrintSpec ps = {d.basename, src, d.n_all, d.flag_io, d.interval, d.iflux, (int64_t)c.forc_start_time,
                             c.binary, c.ascii, c.radiation_input_mode, c.terrain_radiation,
                             lonlat_name(c.solar_lonlat_mode), c.solar_lon_deg, c.solar_lat_deg};
         if (shud_out_add(out, &ps)) {
@@ -176,6 +176,12 @@ int main(int argc, char **argv) {
             ShudEtForcing f;
             if (shud_project_forcing(p, t, tout, &f)) {
                 fprintf(stderr, "%s\n", shud_project_error());
+                rc = 1;
+                break;
+            }
+            ShudStepInputs bc = {};                 // tsd_eyBC .. tsd_rqBC rows (f_update's getX)
+            if (shud_project_bc_rows(p, &bc) == 1 && shud_rhs_set_step_inputs(h, &bc)) {
+                fprintf(stderr, "shud_rhs_set_step_inputs (BC rows): %s\n", shud_rhs_last_error_string());
                 rc = 1;
                 break;
             }

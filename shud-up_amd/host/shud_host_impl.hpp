@@ -61,6 +61,12 @@ struct Project {
     std::vector<Series> wx;
     Series lai, mf;
     bool have_lai = false, have_mf = false;
+    // boundary-condition series (tsd.ebc1 / ebc2 / rbc1 / rbc2) and their padded rows, and cfg.output flags
+    Series bc[4];
+    bool have_bc[4] = {false, false, false, false};
+    int bc_w[4] = {0, 0, 0, 0};
+    std::vector<double> bc_row[4];
+    std::vector<int32_t> io_ele, io_riv, io_lake;
     // TSR bucket (MD_ET.cpp:60-136)
     long long tsr_bucket = -1;
     double tsr_t0 = 0, tsr_t1 = 0;
@@ -81,6 +87,9 @@ bool read_table(FILE *fp, Table &t);
 int load(Project &p, const char *indir, const char *prj, const char *cwd, double end_day);
 int read_forcing(Project &p, const char *cwd);
 int step_forcing(Project &p, double t, double tout, ShudEtForcing *f);
+int read_bc(Project &p);
+int read_series_file(Project &p, Series &s);
+int move_series(Project &p, Series &s, double t);
 void solar_position(const Project &p, double t_min, double lat_deg, double lon_deg, double tz, bool tz_given,
                     double out[5]);
 

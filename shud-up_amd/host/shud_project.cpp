@@ -28,7 +28,7 @@ int fail(Project *p, const char *fmt, ...) {
 }
 const char *last_error() { return g_err.c_str(); }
 
-static constexpr int kMaxLen = 1024;             // MAXLEN (Macros.hpp)
+static constexpr int kMaxLen = 2048;             // MAXLEN (Macros.hpp:30)
 static constexpr double kMinRivSlope = 4e-4;     // MINRIVSLOPE (Macros.hpp:47)
 static constexpr double kZero = 1.0e-10;         // ZERO (Macros.hpp:32)
 static constexpr double kHeightWind = 10;        // HeightWindMeasure (Macros.hpp:71)
@@ -369,10 +369,6 @@ int load(Project &p, const char *indir, const char *prj, const char *cwd, double
         p.iss[i] = (int32_t)att.at(i, 7);
         p.ilake[i] = (int32_t)att.at(i, 8);
     }
-    for (int i = 0; i < NE; i++)
-        if (p.ibc[i] != 0)
-            return fail(&p, "element %d: iBC = %d needs the .tsd.ebc1/.tsd.ebc2 tables, which this host does not read",
-                        i + 1, p.ibc[i]);
     // segments -> RivID (MD_initialize.cpp:188-191), rmSinks (Model_Data.cpp:238-266): one pass in element
     // order, a raised element is seen raised by the later ones; then InitElement again
     std::vector<int> riv_id(NE, 0);
@@ -430,9 +426,6 @@ int load(Project &p, const char *indir, const char *prj, const char *cwd, double
         if (rt[r] < 0 || rt[r] >= nrt) return fail(&p, "river reach %d: type out of range", r + 1);
         p.riv_down[r] = down > 0 ? down - 1 : down;
         p.riv_bc[r] = (int32_t)riv.at(r, 5);
-        if (p.riv_bc[r] != 0)
-            return fail(&p, "river reach %d: BC = %d needs the .tsd.rbc1/.tsd.rbc2 tables, which this host does not read",
-                        r + 1, p.riv_bc[r]);
         p.riv_length[r] = riv.at(r, 4);
         p.riv_slope[r] = rmax(kMinRivSlope, riv.at(r, 3));
         rrough[r] = R_rough[rt[r]];
@@ -510,6 +503,34 @@ int load(Project &p, const char *indir, const char *prj, const char *cwd, double
             fclose(fp);
         }
     }
+    // read_cfgout (MD_readin.cpp:25-104): all columns on unless <prj>.cfg.output lists them; each table's
+    // header line sets the default (atoi of its text), then "index ON/OFF" rows
+    p.io_ele.assign(NE, 1);
+    p.io_riv.assign(NR, 1);
+    p.io_lake.assign(p.NL, 1);
+    {
+        const std::string fn = path_of(p, "cfg.output");
+        FILE *fp = fopen(fn.c_str(), "r");
+        if (fp) {
+            std::vector<int32_t> *io[3] = {&p.io_ele, &p.io_riv, &p.io_lake};
+            const int n[3] = {NE, NR, p.NL};
+            for (int k = 0; k < 3; k++) {
+                if (k > 0 && n[k] == 0) continue;
+                Table tb;
+                if (!read_table(fp, tb) || tb.ncol != 2) {
+                    fclose(fp);
+                    return fail(&p, "%s: the tables must have 2 columns (index, OFF/ON)", fn.c_str());
+                }
+                io[k]->assign(n[k], atoi(tb.header.c_str()));
+                for (int r = 0; r < tb.nrow; r++) {
+                    const int idx = (int)tb.at(r, 0) - 1;
+                    if (idx >= 0 && idx < n[k]) (*io[k])[idx] = (int)tb.at(r, 1) > 0 ? 1 : 0;
+                }
+            }
+            fclose(fp);
+        }
+    }
+    if (int rc2 = read_bc(p)) return rc2;
     return read_forcing(p, cwd);
 }
 
@@ -608,7 +629,7 @@ const double *shud_project_array(shud_project_t h, const char *name, int64_t *n)
 int shud_project_outputs(shud_project_t h, const char *outdir, ShudOutputDecl *decl, int max) {
     if (!h || !outdir) return fail(nullptr, "null argument");
     Project &p = *reinterpret_cast<Project *>(h);
-    struct D { std::string sfx; int arr, col, n, dt, flux; };
+    struct D { std::string sfx; int arr, col, n, dt, flux; };   // n: NumEle / NumRiv / NumLake control
     std::vector<D> v;
     const int NE = p.NE, NR = p.NR, NL = p.NL;
     auto add = [&](const char *sfx, int arr, int n, int dt, int flux, int col = -1) {
@@ -655,7 +676,16 @@ int shud_project_outputs(shud_project_t h, const char *outdir, ShudOutputDecl *d
     if (p.dt_Qr_sub > 0) add("rivqsub", SHUD_ARR_QRIV_SUB, NR, p.dt_Qr_sub, 1);
     if (p.dt_Qr_surf > 0) add("rivqsurf", SHUD_ARR_QRIV_SURF, NR, p.dt_Qr_surf, 1);
     if (p.dt_yr_stage > 0) add("rivystage", SHUD_ARR_Y_RIV_STG, NR, p.dt_yr_stage, 0);
-    if (p.dt_lake > 0 && NL > 0) add("lakystage", SHUD_ARR_Y_LAKE_STG, NL, p.dt_lake, 0);
+    if (p.dt_lake > 0 && NL > 0) {
+        add("lakystage", SHUD_ARR_Y_LAKE_STG, NL, p.dt_lake, 0);
+        add("lakatop", SHUD_ARR_LAKE_TOPAREA, NL, p.dt_lake, 0);
+        add("lakvevap", SHUD_ARR_Q_LAKE_EVAP, NL, p.dt_lake, 1);
+        add("lakvprcp", SHUD_ARR_Q_LAKE_PRCP, NL, p.dt_lake, 1);
+        add("lakqrivin", SHUD_ARR_Q_LAKE_RIVIN, NL, p.dt_lake, 1);
+        add("lakqrivout", SHUD_ARR_Q_LAKE_RIVOUT, NL, p.dt_lake, 1);
+        add("lakqsurf", SHUD_ARR_Q_LAKE_SURF, NL, p.dt_lake, 1);
+        add("lakqsub", SHUD_ARR_Q_LAKE_SUB, NL, p.dt_lake, 1);
+    }
     p.out_names.clear();
     for (auto &d : v) p.out_names.push_back(std::string(outdir) + "/" + p.prj + "." + d.sfx);
     const int n = (int)v.size();
@@ -666,6 +696,14 @@ int shud_project_outputs(shud_project_t h, const char *outdir, ShudOutputDecl *d
         decl[k].n_all = v[k].n;
         decl[k].interval = v[k].dt;
         decl[k].iflux = v[k].flux;
+        // io_ele / io_riv / io_lake by the control's size, as initialize_output passes them
+        const int a = v[k].arr;
+        const bool lake = a == SHUD_ARR_Y_LAKE_STG || (a >= SHUD_ARR_LAKE_TOPAREA && a <= SHUD_ARR_Q_LAKE_SUB);
+        const bool riv = a == SHUD_ARR_Y_RIV_STG || (a >= SHUD_ARR_QRIV_DOWN && a <= SHUD_ARR_QRIV_SUB);
+        const std::vector<int32_t> &io = lake ? p.io_lake : riv ? p.io_riv : p.io_ele;
+        bool all = true;
+        for (int32_t f : io) all = all && f;
+        decl[k].flag_io = all ? nullptr : io.data();
     }
     return n;
 }
@@ -673,6 +711,23 @@ int shud_project_outputs(shud_project_t h, const char *outdir, ShudOutputDecl *d
 int shud_project_forcing(shud_project_t h, double t, double tout, ShudEtForcing *f) {
     if (!h || !f) return fail(nullptr, "null argument");
     return step_forcing(*reinterpret_cast<Project *>(h), t, tout, f);
+}
+
+int shud_project_bc_rows(shud_project_t h, ShudStepInputs *in) {
+    if (!h || !in) return fail(nullptr, "null argument");
+    Project &p = *reinterpret_cast<Project *>(h);
+    const double **rows[4] = {&in->ele_ybc, &in->ele_qbc, &in->riv_ybc, &in->riv_qbc};
+    int32_t *ns[4] = {&in->n_ele_ybc, &in->n_ele_qbc, &in->n_riv_ybc, &in->n_riv_qbc};
+    int any = 0;
+    for (int k = 0; k < 4; k++) {
+        if (!p.have_bc[k]) continue;
+        p.bc_row[k].assign(p.bc_w[k], 0.0);
+        memcpy(p.bc_row[k].data(), p.bc[k].row(), p.bc[k].ncol * sizeof(double));
+        *rows[k] = p.bc_row[k].data();
+        *ns[k] = p.bc_w[k] - 1;                      // data columns (x[0] is the time column)
+        any = 1;
+    }
+    return any;
 }
 
 int shud_project_solar(shud_project_t h, double t_min, double lat, double lon, double tz, double *out5) {

@@ -214,7 +214,8 @@ ODE_FUNCTIONS = {
  SHUD_ARR_QE2R_SUB, SHUD_ARR_Q_INFIL, SHUD_ARR_Q_EXFIL, SHUD_ARR_Q_RECHARGE, SHUD_ARR_Q_ETA, SHUD_ARR_Q_E_IC,
  SHUD_ARR_Q_TRANS, SHUD_ARR_Q_EVAPO, SHUD_ARR_QRIV_DOWN, SHUD_ARR_QRIV_UP, SHUD_ARR_QRIV_SURF, SHUD_ARR_QRIV_SUB,
  SHUD_ARR_Q_PRCP, SHUD_ARR_Q_NET_PRCP, SHUD_ARR_Q_ETP, SHUD_ARR_Y_ELE_IS, SHUD_ARR_Y_ELE_SNOW, SHUD_ARR_RN_H,
- SHUD_ARR_RN_T, SHUD_ARR_RN_FACTOR, SHUD_ARR_COUNT) = range(31)
+ SHUD_ARR_RN_T, SHUD_ARR_RN_FACTOR, SHUD_ARR_LAKE_TOPAREA, SHUD_ARR_Q_LAKE_EVAP, SHUD_ARR_Q_LAKE_PRCP,
+ SHUD_ARR_Q_LAKE_RIVIN, SHUD_ARR_Q_LAKE_RIVOUT, SHUD_ARR_Q_LAKE_SURF, SHUD_ARR_Q_LAKE_SUB, SHUD_ARR_COUNT) = range(38)
 
 
 class ShudPrintSpec(C.Structure):

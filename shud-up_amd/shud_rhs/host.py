@@ -33,7 +33,7 @@ class ShudControl(C.Structure):
 
 class ShudOutputDecl(C.Structure):
     _fields_ = [("basename", C.c_char_p), ("array", C.c_int32), ("column", C.c_int32), ("n_all", C.c_int32),
-                ("interval", C.c_int32), ("iflux", C.c_int32)]
+                ("interval", C.c_int32), ("iflux", C.c_int32), ("flag_io", C.POINTER(C.c_int32))]
 
 
 _H = C.c_void_p
@@ -55,6 +55,7 @@ def lib():
             "shud_project_array": (C.POINTER(C.c_double), [_H, C.c_char_p, C.POINTER(C.c_int64)]),
             "shud_project_outputs": (C.c_int, [_H, C.c_char_p, C.POINTER(ShudOutputDecl), C.c_int]),
             "shud_project_forcing": (C.c_int, [_H, C.c_double, C.c_double, C.POINTER(abi.ShudEtForcing)]),
+            "shud_project_bc_rows": (C.c_int, [_H, C.POINTER(abi.ShudStepInputs)]),
             "shud_project_solar": (C.c_int, [_H, C.c_double, C.c_double, C.c_double, C.c_double,
                                              C.POINTER(C.c_double)]),
         }
@@ -147,7 +148,22 @@ class Project:
         arr = (ShudOutputDecl * max(n, 1))()
         lib().shud_project_outputs(self.h, outdir, arr, n)
         return [{"basename": d.basename.decode(), "array": d.array, "column": d.column, "n_all": d.n_all,
-                 "interval": d.interval, "iflux": d.iflux} for d in arr[:n]]
+                 "interval": d.interval, "iflux": d.iflux,
+                 "flag_io": None if not d.flag_io else _arr(d.flag_io, d.n_all, np.int32)} for d in arr[:n]]
+
+    def bc_rows(self):
+        """{ele_ybc, ele_qbc, riv_ybc, riv_qbc} rows at the current ET step (model.step_struct bc_tables form:
+        x[0] = time, x[c] = column c), or {} without boundary conditions"""
+        s = abi.ShudStepInputs()
+        if lib().shud_project_bc_rows(self.h, C.byref(s)) != 1:
+            return {}
+        out = {}
+        for k in ("ele_ybc", "ele_qbc", "riv_ybc", "riv_qbc"):
+            n = getattr(s, "n_" + k)
+            p = getattr(s, k)
+            if p and n > 0:
+                out[k] = _arr(p, n + 1, np.float64)
+        return out
 
     def forcing(self, t, tout):
         """EtForcing for the ET step [t, tout) (advances the series pointers: call in time order)."""

@@ -223,11 +223,24 @@ def synth_raw(n_target, seed=12345, h=100.0, stem_every=12, reach_quads=3):
 
 
 def write_project(outdir, prj, n_target, days=2.0, seed=12345, max_step=10.0, et_step=60.0, dt_out=60,
-                  forcing_dt_min=60.0, extra_para=None):
-    """Write input files <outdir>/<prj>.* for the synthetic mesh; returns the in-memory ShudModel."""
+                  forcing_dt_min=60.0, extra_para=None, bc=False, cfg_output=False):
+    """Write input files <outdir>/<prj>.* for the synthetic mesh; returns the in-memory ShudModel.
+    bc: a few elements / reaches get boundary conditions (iBC = +-1, +-2; BC = +-1) with hourly .tsd.ebc1/.ebc2/
+    .rbc1/.rbc2 tables.  cfg_output: a .cfg.output switching some element / reach columns off."""
     os.makedirs(outdir, exist_ok=True)
     m, raw = synth_raw(n_target, seed=seed)
     NE, NR, NS = m.num_ele, m.num_riv, m.num_seg
+    ibc = np.zeros(NE, dtype=np.int64)
+    rbc = np.zeros(NR, dtype=np.int64)
+    if bc:
+        rng_bc = np.random.default_rng(seed + 7)
+        riv_ele = np.zeros(NE, dtype=bool)
+        riv_ele[m.seg_ele] = True
+        cand = np.nonzero(~riv_ele)[0]
+        pick_e = rng_bc.choice(cand, 8, replace=False)
+        ibc[pick_e] = [1, 2, 1, 2, -1, -2, -1, -2]
+        pick_r = rng_bc.choice(NR, 4, replace=False)
+        rbc[pick_r] = [1, -1, 1, -1]
     p = lambda ext: os.path.join(outdir, f"{prj}.{ext}")
     nbr = m.nabr.reshape(3, NE)
     with open(p("sp.mesh"), "w") as f:
@@ -238,7 +251,7 @@ def write_project(outdir, prj, n_target, days=2.0, seed=12345, max_step=10.0, et
     pick = raw["pick"]
     with open(p("sp.att"), "w") as f:
         _write_table(f, ["INDEX", "SOIL", "GEOL", "LC", "FORC", "MF", "BC", "SS", "LAKE"],
-                     ([i + 1, pick[i, 0], pick[i, 1], pick[i, 2], 1, 1, 0, 0, 0] for i in range(NE)))
+                     ([i + 1, pick[i, 0], pick[i, 1], pick[i, 2], 1, 1, ibc[i], 0, 0] for i in range(NE)))
     for ext, tab in (("para.soil", raw["soil"]), ("para.geol", raw["geol"]), ("para.lc", raw["lc"])):
         with open(p(ext), "w") as f:
             _write_table(f, [f"C{j}" for j in range(tab.shape[1])], ([int(r[0])] + [float(v) for v in r[1:]] for r in tab))
@@ -251,7 +264,7 @@ def write_project(outdir, prj, n_target, days=2.0, seed=12345, max_step=10.0, et
     with open(p("sp.riv"), "w") as f:
         _write_table(f, ["Index", "Down", "Type", "Slope", "Length", "BC"],
                      ([r + 1, down[r] + 1 if down[r] >= 0 else down[r], rt[r] + 1, float(m.riv["riv_bed_slope"][r]),
-                       float(m.riv["riv_length"][r]), 0] for r in range(NR)))
+                       float(m.riv["riv_length"][r]), rbc[r]] for r in range(NR)))
         _write_table(f, ["Index", "Depth", "BankSlope", "Width", "Sinuosity", "Manning", "Cwr", "KsatH", "BedThick"],
                      ([int(r[0])] + [float(v) for v in r[1:]] for r in R))
     with open(p("sp.rivseg"), "w") as f:
@@ -295,6 +308,29 @@ def write_project(outdir, prj, n_target, days=2.0, seed=12345, max_step=10.0, et
     with open(p("tsd.forc"), "w") as f:
         f.write("1 20000101\n\nID\tLon\tLat\tX\tY\tZ\tFilename\n")
         f.write("1\t-122.71\t39.195\t0\t0\t-9999\tforcing.csv\n")
+    if bc:
+        # hourly BC tables: element heads (ebc1, m), element fluxes (ebc2, m3/min), river stages / fluxes
+        nh = int(np.ceil(days * 24)) + 2
+        aqm = float(np.median(m.par["aquifer_depth"]))
+        tabs = {"tsd.ebc1": [0.5 * aqm + 0.1 * np.sin(np.arange(nh) / 5.0), 0.7 * aqm + 0.05 * np.cos(np.arange(nh) / 7.0)],
+                "tsd.ebc2": [-0.02 + 0.01 * np.sin(np.arange(nh) / 3.0), 0.03 + 0.0 * np.arange(nh)],
+                "tsd.rbc1": [0.8 + 0.2 * np.sin(np.arange(nh) / 4.0)],
+                "tsd.rbc2": [5.0 + 2.0 * np.cos(np.arange(nh) / 6.0)]}
+        for ext, cols in tabs.items():
+            with open(p(ext), "w") as f:
+                f.write(f"{nh}\t{len(cols) + 1}\t20000101\n")
+                f.write("Time_Day\t" + "\t".join(f"X{j + 1}" for j in range(len(cols))) + "\n")
+                for k in range(nh):
+                    f.write(f"{k / 24.0:.17g}\t" + "\t".join(f"{c[k]:.17g}" for c in cols) + "\n")
+    if cfg_output:
+        with open(p("cfg.output"), "w") as f:
+            # element table: header default 1 (atoi of "1 ..."), a few columns off; river table: default 0
+            off = np.arange(0, NE, max(1, NE // 7))
+            _write_table(f, ["1", "ON"], ([int(i) + 1, 0] for i in off))
+            on = np.arange(0, NR, max(1, NR // 5))
+            f.write(f"{len(on)}\t2\n0\tON\n")
+            for r in on:
+                f.write(f"{int(r) + 1}\t1\n")
     nlc = raw["lc"].shape[0]
     months = int(days // 31) + 3
     with open(p("tsd.lai"), "w") as f:

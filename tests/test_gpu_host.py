@@ -40,9 +40,17 @@ def _device_model(P):
     return m, h
 
 
-def test_shud_gpu_matches_python_driver(tmp_path):
+@pytest.mark.parametrize("case", ["plain", "bc_substep"])
+def test_shud_gpu_matches_python_driver(tmp_path, case):
+    """plain: 10-min solver steps, ET every step.  bc_substep: element/river boundary-condition tables
+    (.tsd.ebc1/.ebc2/.rbc1/.rbc2 rows through shud_project_bc_rows), a .cfg.output column selection, and ET
+    sub-stepping (ETStep 10 < SolverStep 30: CVodeSetStopTime per ET step, shud.cpp:86-87,112-115)."""
     src = tmp_path / "in"
-    synth.write_project(str(src), "syn", 2000, days=1.0, max_step=10.0, et_step=60.0, dt_out=60)
+    if case == "plain":
+        synth.write_project(str(src), "syn", 2000, days=1.0, max_step=10.0, et_step=60.0, dt_out=60)
+    else:
+        synth.write_project(str(src), "syn", 2000, days=1.0, max_step=30.0, et_step=10.0, dt_out=60, bc=True,
+                            cfg_output=True)
     out_c, out_p = tmp_path / "out_cpp", tmp_path / "out_py"
     r = subprocess.run([SHUD_GPU, "-o", str(out_c), "-C", str(src), str(src), "syn"], capture_output=True,
                        text=True, timeout=240)
@@ -62,10 +70,19 @@ def test_shud_gpu_matches_python_driver(tmp_path):
         if d["column"] >= 0:
             p += 8 * d["column"] * m.num_ele
         out.add(d["basename"], p, d["n_all"], d["interval"], d["iflux"], start_time=c["forc_start_time"],
+                flag_io=d["flag_io"],
                 binary=bool(c["binary"]), ascii=bool(c["ascii"]), radiation_input_mode=c["radiation_input_mode"],
                 terrain_radiation=c["terrain_radiation"], solar_lonlat_mode=LONLAT[c["solar_lonlat_mode"]],
                 lon=c["solar_lon_deg"], lat=c["solar_lat_deg"])
-    t, _ = sv.run(c["num_steps"], forcing=P.forcing, output=out)
+    def forcing(t, tout):                       # shud_gpu.cpp: forcing rows, then the BC rows, then ET
+        f = P.forcing(t, tout)
+        bc = P.bc_rows()
+        if bc:
+            h.set_step_inputs(step={}, bc_tables=bc)
+        return f
+
+    assert (len(P.bc_rows()) == 4) == (case == "bc_substep")
+    t, _ = sv.run(c["num_steps"], forcing=forcing, output=out)
     assert abs(t - c["end_time"]) < 1e-6
     out.close()
     files = sorted(os.path.basename(f) for f in glob.glob(str(out_c / "*.dat")))
@@ -76,9 +93,12 @@ def test_shud_gpu_matches_python_driver(tmp_path):
         assert a == b, f
         d = shudio.read_dat(str(out_c / f))
         assert d["t"].size == 24 and np.all(np.isfinite(d["data"])), f
+        if case != "plain" and ".riv" in f:
+            assert d["data"].shape[1] < m.num_riv                  # cfg.output selection
         assert np.array_equal(d["t"], np.arange(24) * 60.0)
-    gw = shudio.read_dat(str(out_c / "syn.eleygw.dat"))["data"]
-    assert np.abs(gw - P.array("y0")[2 * m.num_ele:3 * m.num_ele]).max() < 1.0    # one day moves gw < 1 m
+    if case == "plain":
+        gw = shudio.read_dat(str(out_c / "syn.eleygw.dat"))["data"]
+        assert np.abs(gw - P.array("y0")[2 * m.num_ele:3 * m.num_ele]).max() < 1.0    # one day moves gw < 1 m
     sv.close()
     h.close()
 

@@ -176,3 +176,32 @@ def test_tsr_buckets(tmp_path):
         assert np.array_equal(f.tsr[2], sz) and np.array_equal(f.tsr[3], wd) and f.tsr_den == den, t
     assert modes[:6] == [abi.SHUD_TSR_RECOMPUTE, abi.SHUD_TSR_CACHED, abi.SHUD_TSR_CACHED] * 2
     assert max(dens) > 0 and min(dens) == 0.0                # daytime and night-time intervals both covered
+
+
+def test_boundary_condition_rows_and_cfg_output(tmp_path):
+    """read_bcEle1/2, read_bcRiv1/2 (MD_readin.cpp:959-982) with the zero-order hold f_update reads through
+    getX (MD_update.cpp:114-125, 145-160); read_cfgout's column flags (MD_readin.cpp:25-104)."""
+    synth.write_project(str(tmp_path), "syn", 900, days=1.0, bc=True, cfg_output=True)
+    P = host.Project(str(tmp_path), "syn", cwd=str(tmp_path))
+    m = P.model()
+    tabs = {k: _csv_rows(os.path.join(tmp_path, f"syn.tsd.{e}"))
+            for k, e in (("ele_ybc", "ebc1"), ("ele_qbc", "ebc2"), ("riv_ybc", "rbc1"), ("riv_qbc", "rbc2"))}
+    for t in np.arange(0.0, 1440.0, 45.0):
+        P.forcing(t, t + 45.0)
+        rows = P.bc_rows()
+        assert set(rows) == set(tabs)
+        for k, tab in tabs.items():
+            r = np.nonzero(tab[:, 0] <= t)[0][-1]
+            assert np.array_equal(rows[k], tab[r]), (k, t)
+    assert sorted(set(m.ibc.tolist())) == [-2, -1, 0, 1, 2] and sorted(set(m.riv_bc.tolist())) == [-1, 0, 1]
+    outs = P.outputs(str(tmp_path / "out"))
+    ele = next(o for o in outs if o["basename"].endswith(".eleygw"))
+    riv = next(o for o in outs if o["basename"].endswith(".rivystage"))
+    NE, NR = m.num_ele, m.num_riv
+    off = np.arange(0, NE, max(1, NE // 7))
+    want = np.ones(NE, dtype=np.int32)
+    want[off] = 0
+    assert np.array_equal(ele["flag_io"], want)
+    want = np.zeros(NR, dtype=np.int32)
+    want[np.arange(0, NR, max(1, NR // 5))] = 1
+    assert np.array_equal(riv["flag_io"], want)
