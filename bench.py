@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--host-vectors", action="store_true", help="also time the PCIe-inclusive host-vector eval")
     ap.add_argument("--no-et", action="store_true", help="skip the ET-step prelude timing (SURVEY f1)")
     ap.add_argument("--no-ode", action="store_true", help="skip the device integrator timing (SURVEY f2)")
+    ap.add_argument("--e2e-ele", type=int, default=100_000,
+                    help="elements of the end-to-end shud_gpu run (C++ host, one simulated day); 0 = skip")
     ap.add_argument("--partition-1", action="store_true",
                     help="run the N>1 code path (partitioned handle, RCCL comm, overlap) with one rank (smoke test)")
     args = ap.parse_args()
@@ -192,6 +194,8 @@ def main():
 
     if world == 1 and not args.no_et:
         out["et_prelude"] = et_prelude_timing(h, gm)
+    if world == 1 and rank == 0 and args.e2e_ele > 0:
+        out["end_to_end"] = e2e_timing(args.e2e_ele)
     if world == 1 and not args.no_ode:
         out["integrator"] = ode_timing(h, y_glob, ms_eval)
 
@@ -204,6 +208,28 @@ def main():
     h.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def e2e_timing(n_ele, days=1.0):
+    """SHUD() end to end through the C++ host (shud-up_amd/shud_gpu): a synthetic project written
+    in SHUD text format (seeded mesh + river tree, hourly forcing, 24 hourly outputs), run for `days` simulated
+    days as a child process; its own timing line is reported (loop_s = the time loop, wall_s incl. load)."""
+    import subprocess
+    import tempfile
+    from shud_rhs import synth
+    exe = os.path.join(ROOT, "shud-up_amd", "shud_gpu")
+    with tempfile.TemporaryDirectory() as d:
+        synth.write_project(d, "syn", n_ele, days=days)
+        r = subprocess.run([exe, "-q", "-o", os.path.join(d, "out"), "-C", d, d, "syn"], capture_output=True,
+                           text=True, timeout=300)
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith('{"shud_gpu"')]
+        if r.returncode != 0 or not line:
+            return {"error": f"shud_gpu exit {r.returncode}: {(r.stderr or r.stdout)[-300:]}"}
+        res = json.loads(line[-1])["shud_gpu"]
+    res["simulated_days_per_s"] = days / res["loop_s"] if res["loop_s"] > 0 else None
+    res["note"] = ("shud_gpu (C++ host: readers, forcing/TSR, device ET prelude + RHS + integrator + outputs) on a "
+                   f"synthetic {n_ele}-element project, {days:g} simulated day(s), hourly forcing and outputs")
+    return res
 
 
 def ode_timing(h, y0, ms_eval, max_steps=40, budget_s=4.0):
