@@ -5,7 +5,7 @@ Workload (BASELINE.json north_star / SURVEY §8d): synthetic 10M-triangle mesh (
 ccw-like river density, seed 12345), seeded random state y and ET-step inputs, serial (reference `make
 shud`) semantics.  One "step" = one RHS evaluation f(t, y, ydot) with y / ydot resident in HBM.
 N = 1: the whole mesh on one GPU.  N > 1 (torch.distributed.run, one process per GPU): the same 10M mesh
-partitioned by RCB across the N ranks, ghost states exchanged by RCCL (grouped send/recv over xGMI) inside
+partitioned by the C++ partitioner (multilevel or RCB, whichever gives the smaller largest halo) across the N ranks, ghost states exchanged by RCCL (grouped send/recv over xGMI) inside
 every RHS call; value = NumEle_total x K / max-over-ranks time ("scaling": "strong": the 10M mesh is fixed).
 
 Prints ONE JSON line on rank 0 with roofline (dominant kernel: shud_ele_kernel, HIP-event timed on the
@@ -42,8 +42,10 @@ def main():
     ap.add_argument("--mode", choices=["serial", "omp"], default="serial")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--profile-reps", type=int, default=20)
-    ap.add_argument("--host-vectors", action="store_true", help="also time the PCIe-inclusive host-vector eval")
+    ap.add_argument("--profile-reps", type=int, default=20, help="N>1: serialized per-phase timing reps")
+    ap.add_argument("--no-host-vectors", action="store_true", help="skip the PCIe-inclusive host-vector eval")
+    ap.add_argument("--no-many-class", action="store_true",
+                    help="skip the many-parameter-class workloads (L2 class table, SoA fallback)")
     ap.add_argument("--no-et", action="store_true", help="skip the ET-step prelude timing (SURVEY f1)")
     ap.add_argument("--no-ode", action="store_true", help="skip the device integrator timing (SURVEY f2)")
     ap.add_argument("--e2e-ele", type=int, default=100_000,
@@ -76,9 +78,17 @@ def main():
 
     stream = torch.cuda.current_stream()
     if world > 1 or args.partition_1:
-        ele_part, _, plans = partition.build_plans(gm, world)
-        cut_e, cut_s = partition.edge_cut(gm, ele_part)
-        lm, part = partition.local_model(gm, plans[rank], rank, world)
+        # the C++ partitioner + planner (include/shud_partition.h): multilevel and RCB, the smaller largest
+        # halo wins; every rank computes the same partition (deterministic), then only its own plan
+        tp = time.time()
+        ele_part, pst = partition.cpp_partition(gm, world, partition.PART_AUTO, seed=12345)
+        cut_e, cut_s = pst["edge_cut"], pst["segment_cut"]
+        plan = partition.CppPlan(gm, ele_part, world, rank)
+        lm, part = plan.local_model()
+        plan.close()
+        log(f"[bench] C++ partition ({'multilevel' if pst['method_used'] == 0 else 'RCB'}, "
+            f"{pst['seconds']:.1f}s) + plan/local mesh in {time.time() - tp:.1f}s; largest halo "
+            f"{pst['max_halo']} entities")
         uid = [runtime.nccl_unique_id() if rank == 0 else None]
         if world > 1:
             dist.broadcast_object_list(uid, src=0)
@@ -86,7 +96,7 @@ def main():
         h = runtime.RhsHandle(lm, mode=mode, device=local, stream=stream.cuda_stream, partition=part)
         y_loc = partition.local_state(y_glob, gm, part)
         model = lm
-        log(f"[bench] RCB {world}-way: edge cut {cut_e} mesh edges, {cut_s} river segments; rank0 "
+        log(f"[bench] {world}-way: edge cut {cut_e} mesh edges, {cut_s} river segments; rank0 "
             f"own {part.n_own_ele} ele / {part.n_own_riv} riv, "
             f"ghosts {lm.num_ele - part.n_own_ele} ele / {lm.num_riv - part.n_own_riv} riv")
     else:
@@ -101,6 +111,10 @@ def main():
     for _ in range(args.warmup):
         h.eval_device(0.0, yp, dyp)
     torch.cuda.synchronize()
+    # HIP events around the kernels of every 5th timed eval (handle's stream = torch's current stream): an event
+    # between two kernels stops their tails overlapping, so only a sample of the K evals carries them
+    t_stride = 5 if args.steps >= 20 else 1
+    h.timing(args.steps, t_stride)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -112,6 +126,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t_start
+    ms_ele_loop, ms_riv_loop, ms_eval_loop, n_timed = h.timing_read()
     if world > 1:
         tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -120,9 +135,13 @@ def main():
     if err["exit_code"]:
         log(f"[bench] WARNING physics error flags {err}")
 
-    # per-kernel HIP-event timing on the handle's stream (= torch's current stream)
-    ms_eval, per = h.time_kernels(0.0, yp, dyp, args.profile_reps)
-    if world > 1:
+    # per-kernel times: HIP events recorded inside the timed loop on the handle's stream (= torch's current
+    # stream); a partitioned handle also gets a serialized per-phase breakdown (halo exchange alone)
+    per = {"shud_ele_kernel": ms_ele_loop, "shud_riv_kernel": ms_riv_loop}
+    ms_eval = ms_eval_loop
+    if world > 1 and args.profile_reps > 0:
+        _, per_ser = h.time_kernels(0.0, yp, dyp, args.profile_reps)
+        per["halo_exchange_serialized"] = per_ser.get("halo_exchange")
         dist.barrier()
     ms_ele = per["shud_ele_kernel"]
     ms_riv = per["shud_riv_kernel"]
@@ -150,8 +169,10 @@ def main():
         "data": "synthetic (seeded jittered-grid Delaunay mesh + river tree, random y and ET-step inputs)",
         "config": {"workload": f"syn-10M RHS ({args.mode} semantics)" if NE >= 9_000_000 else f"syn-{NE} RHS",
                    "num_ele": NE, "num_riv": NR, "num_seg": NS,
-                   "parallelism": f"mesh-partition x{world} (RCB, RCCL halo)" if world > 1 else "single GPU",
-                   **({"edge_cut": cut_e, "segment_cut": cut_s} if world > 1 else {}),
+                   "parallelism": (f"mesh-partition x{world} (C++ {'multilevel' if pst['method_used'] == 0 else 'RCB'}"
+                                   f" partition, RCCL halo)") if world > 1 else "single GPU",
+                   **({"edge_cut": cut_e, "segment_cut": cut_s, "max_halo_entities": pst["max_halo"],
+                       "imbalance": pst["imbalance"]} if world > 1 else {}),
                    "y_ydot": "device-resident"},
         "roofline": {
             "bound": "hbm",
@@ -163,26 +184,29 @@ def main():
             "traffic": None,
             "algorithmic_bytes_per_launch": ele_bytes,
             "kernel_ms": {k: v for k, v in per.items()},
+            "kernel_ms_source": (f"HIP events around the kernels of {n_timed} of the {args.steps} timed evals "
+                                 f"(every {t_stride}th; handle stream)"),
             "rhs_frac": (ele_bytes + riv_bytes) / (ms_eval * 1e-3) / HBM_PEAK,
+            "riv_algorithmic_bytes_per_launch": riv_bytes,
+            "riv_frac": riv_bytes / (ms_riv * 1e-3) / HBM_PEAK if ms_riv > 0 else None,
         },
         "cpu_baseline": None,
     }
-    # the practical HBM ceiling on this box: a STREAM-copy (torch's device copy kernel, 2 GiB -> 2 GiB)
-    sc = stream_copy_gbs(local)
-    out["roofline"]["stream_copy_GBs"] = sc
-    out["roofline"]["frac_of_stream_copy"] = achieved / 1e9 / sc if sc else None
-    pmc = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    if os.path.exists(pmc) and world == 1:
-        try:
-            with open(pmc) as f:
-                pj = json.load(f)
-            if pj.get("num_ele") == NE and "shud_ele_kernel" in pj.get("kernels", {}):
-                out["roofline"]["traffic"] = pj["kernels"]["shud_ele_kernel"]["hbm_bytes_per_launch"]
-                out["roofline"]["traffic_source"] = "profiles/pmc_summary.json (rocprofv3 --pmc, corrected)"
-        except Exception as e:  # noqa: BLE001
-            log(f"[bench] could not read {pmc}: {e}")
+    # the practical HBM ceilings on this box: STREAM copy and read-only sweeps (libshud_stream.so)
+    sp = stream_probe(local) if world == 1 else {}
+    if sp:
+        out["roofline"].update(sp)
+        out["roofline"]["frac_of_stream_copy"] = achieved / 1e9 / sp["stream_copy_GBs"]
+    if world == 1:
+        tr = pmc_traffic(NE)
+        out["roofline"].update(tr)
+        if out["roofline"].get("traffic"):
+            out["roofline"]["frac_actual"] = out["roofline"]["traffic"] / (ms_ele * 1e-3) / HBM_PEAK
+        rt = tr.get("riv_traffic")
+        if rt and ms_riv > 0:
+            out["roofline"]["riv_frac_actual"] = rt / (ms_riv * 1e-3) / HBM_PEAK
 
-    if args.host_vectors and world == 1:
+    if not args.no_host_vectors and world == 1:
         y_h = np.ascontiguousarray(y_loc)
         dy_h = np.empty_like(y_h)
         h.eval(0.0, y_h, dy_h)
@@ -191,11 +215,25 @@ def main():
         for _ in range(nrep):
             h.eval(0.0, y_h, dy_h, raise_on_physics=False)
         out["host_vector_value"] = NE * nrep / (time.perf_counter() - th)
+        out["host_vector_note"] = ("PCIe-inclusive: y H2D + RHS + ydot D2H + error-word read per eval (the "
+                                   "reference f's host N_Vector contract), never `value`")
 
+    if world == 1 and not args.no_many_class:
+        h.close()                      # free the default handle's device memory first
+        h = None
+        out["many_class"] = many_class_timing(gm, y_glob, mode, local, args.steps)
     if world == 1 and not args.no_et:
+        if h is None:
+            h = runtime.RhsHandle(gm, mode=mode, device=local, stream=stream.cuda_stream)
+            h.set_step_inputs()
+            h.eval_device(0.0, yp, dyp)
         out["et_prelude"] = et_prelude_timing(h, gm)
     if world == 1 and rank == 0 and args.e2e_ele > 0:
         out["end_to_end"] = e2e_timing(args.e2e_ele)
+    if world == 1 and not args.no_ode and h is None:
+        h = runtime.RhsHandle(gm, mode=mode, device=local, stream=stream.cuda_stream)
+        h.set_step_inputs()
+        h.eval_device(0.0, yp, dyp)
     if world == 1 and not args.no_ode:
         out["integrator"] = ode_timing(h, y_glob, ms_eval)
 
@@ -205,7 +243,8 @@ def main():
         dist.barrier()
     if rank == 0:
         print(json.dumps(out), flush=True)
-    h.close()
+    if h is not None:
+        h.close()
     if world > 1:
         dist.destroy_process_group()
 
@@ -280,30 +319,131 @@ def et_prelude_timing(h, gm, reps=10):
                     "plus the host's tReadForcing/ET loops"}
 
 
-def stream_copy_gbs(dev, n=1 << 28, reps=20):
-    """STREAM copy (shud-up_amd/libshud_stream.so: 16-B non-temporal loads/stores, grid-stride), 2 GiB -> 2 GiB,
-    HIP-event timed on torch's current stream: the practical HBM ceiling of this box."""
+def stream_probe(dev, n=1 << 27, reps=20):
+    """STREAM probes (shud-up_amd/libshud_stream.so; configurations from tools/stream_sweep.hip), 1 GiB buffers, HIP-event timed on torch's current stream:
+    the best of three copy kernels (bytes read + written) and a read-only sweep (bytes read): the practical
+    HBM ceilings of this box for a copy and for a read-dominated stream."""
     import ctypes
     import torch
     lib = ctypes.CDLL(os.path.join(ROOT, "shud-up_amd", "libshud_stream.so"))
-    lib.shud_stream_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    lib.shud_stream_copy_v.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                       ctypes.c_int]
     a = torch.ones(n, dtype=torch.float64, device=f"cuda:{dev}")
     b = torch.empty_like(a)
     st = torch.cuda.current_stream().cuda_stream
-    for _ in range(3):
-        lib.shud_stream_copy(a.data_ptr(), b.data_ptr(), 8 * n, st)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
-    e0.record()
-    for _ in range(reps):
-        lib.shud_stream_copy(a.data_ptr(), b.data_ptr(), 8 * n, st)
-    e1.record()
-    torch.cuda.synchronize()
-    ok = bool(torch.equal(a[:1024], b[:1024]))
-    gbs = 2 * 8 * n * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    res = {}
+    for v in (0, 1, 2, 3):
+        for _ in range(3):
+            lib.shud_stream_copy_v(a.data_ptr(), b.data_ptr(), 8 * n, st, v)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(reps):
+            lib.shud_stream_copy_v(a.data_ptr(), b.data_ptr(), 8 * n, st, v)
+        e1.record()
+        torch.cuda.synchronize()
+        sec = e0.elapsed_time(e1) * 1e-3
+        if v < 3:
+            ok = bool(torch.equal(a[:4096], b[:4096])) and bool(torch.equal(a[-4096:], b[-4096:]))
+            res[v] = 2 * 8 * n * reps / sec / 1e9 if ok else None
+            b.zero_()
+        else:
+            res[v] = 8 * n * reps / sec / 1e9
     del a, b
     torch.cuda.empty_cache()
-    return gbs if ok else None
+    names = {0: "grid-stride nt", 1: "one-shot x4 nt-load nt-store", 2: "one-shot x1 nt-store"}
+    best = max((k for k in (0, 1, 2) if res[k]), key=lambda k: res[k], default=None)
+    if best is None:
+        return {}
+    return {"stream_copy_GBs": res[best], "stream_copy_kernel": names[best],
+            "stream_copy_all_GBs": {names[k]: res[k] for k in (0, 1, 2)}, "stream_read_GBs": res[3]}
+
+
+def kernel_src_hash():
+    """sha256 (16 hex) over the sources the RHS kernels are built from: keys profiles/pmc_summary.json so a
+    PMC traffic figure is only reported for the kernel build it was measured on."""
+    import hashlib
+    hh = hashlib.sha256()
+    csrc = os.path.join(ROOT, "shud-up_amd", "csrc")
+    for f in sorted(os.listdir(csrc)):
+        if f.startswith(("shud_ele_packed", "shud_kernels", "shud_dev", "shud_physics", "shud_rhs.cpp",
+                         "shud_handle")):
+            with open(os.path.join(csrc, f), "rb") as fh:
+                hh.update(f.encode() + b"\0" + fh.read())
+    with open(os.path.join(ROOT, "shud-up_amd", "Makefile"), "rb") as fh:
+        hh.update(fh.read())
+    return hh.hexdigest()[:16]
+
+
+def pmc_traffic(NE):
+    """roofline.traffic from profiles/pmc_summary.json (rocprofv3 FETCH_SIZE / WRITE_SIZE passes, gfx950
+    correction, tools/pmc_summary.py) when it was measured on this mesh AND this kernel build; else null."""
+    pmc = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    src = kernel_src_hash()
+    out = {"traffic": None, "kernel_src_hash": src}
+    if not os.path.exists(pmc):
+        out["traffic_note"] = "no PMC summary"
+        return out
+    try:
+        with open(pmc) as f:
+            pj = json.load(f)
+    except Exception as e:  # noqa: BLE001
+        out["traffic_note"] = f"unreadable PMC summary: {e}"
+        return out
+    if pj.get("num_ele") != NE or pj.get("kernel_src_hash") != src:
+        out["traffic_note"] = (f"PMC summary is stale (measured on num_ele {pj.get('num_ele')}, kernel build "
+                               f"{pj.get('kernel_src_hash')}): traffic not reported")
+        return out
+    k = pj.get("kernels", {})
+    if "shud_ele_kernel" in k:
+        out["traffic"] = k["shud_ele_kernel"]["hbm_bytes_per_launch"]
+        out["traffic_source"] = "profiles/pmc_summary.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE; corrected)"
+    if "shud_riv_kernel" in k:
+        out["riv_traffic"] = k["shud_riv_kernel"]["hbm_bytes_per_launch"]
+    return out
+
+
+def many_class_timing(gm, y, mode, dev, steps):
+    """The same syn-10M mesh with per-element calibrated parameters: KsatH perturbed by (1 + 1e-7 k), k =
+    element mod 400, so the distinct parameter tuples (classes) grow from 33 to 13,200 — more than the 128 one
+    workgroup's LDS copy of the class table holds.  "auto": the layout the handle picks (the SoA kernel);
+    "l2_class_table": the packed layout with its class table read from L2 (SHUD_RHS_L2_CLASS=1).  Timed like
+    the headline (device-resident y, K evals)."""
+    import copy
+    import torch
+    from shud_rhs import runtime
+    res = {}
+    base = gm.par["KsatH"]
+    y_t = torch.from_numpy(y).to(f"cuda:{dev}")
+    dy_t = torch.empty_like(y_t)
+    m2 = copy.copy(gm)
+    m2.par = dict(gm.par)
+    m2.par["KsatH"] = base * (1.0 + 1e-7 * (np.arange(gm.num_ele) % 400))
+    for name, env in (("auto", None), ("l2_class_table", "1")):
+        if env:
+            os.environ["SHUD_RHS_L2_CLASS"] = env
+        try:
+            h = runtime.RhsHandle(m2, mode=mode, device=dev, stream=torch.cuda.current_stream().cuda_stream)
+        finally:
+            os.environ.pop("SHUD_RHS_L2_CLASS", None)
+        h.set_step_inputs()
+        lay = h.layout()
+        for _ in range(3):
+            h.eval_device(0.0, y_t.data_ptr(), dy_t.data_ptr())
+        h.timing(steps, 5 if steps >= 20 else 1)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            h.eval_device(0.0, y_t.data_ptr(), dy_t.data_ptr())
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        me, mr, mv, n = h.timing_read()
+        h.close()
+        res[name] = {"layout": "packed" if lay["packed"] else "soa", "n_classes": 13200 if not lay["packed"]
+                     else lay["n_classes"], "value": gm.num_ele * steps / dt, "ms_per_step": dt / steps * 1e3,
+                     "ele_kernel_ms": me, "riv_kernel_ms": mr}
+    torch.cuda.empty_cache()
+    return res
 
 
 def cpu_baseline(gm, y, mode, budget_s):

@@ -204,6 +204,13 @@ void *shud_rhs_stream(shud_rhs_t h);
  * names_out (comma separated).  Returns wall ms per eval in *ms_eval. */
 int  shud_rhs_time_kernels(shud_rhs_t h, double t, const double *d_y, double *d_ydot, int reps,
                            double *ms_eval, double *ms_out, int *nk, char *names_out, int names_len);
+/* In-loop timing of ordinary evals: while enabled, every `stride`-th eval (up to `max_evals` of them)
+ * records HIP events on the handle's stream before its first launch, after its element kernel(s) and
+ * after its river (+lake) kernel (an event between two kernels keeps them from overlapping, so sampling
+ * keeps the timed loop's throughput intact).  _read returns the per-eval averages (ms) and disables it.
+ * For a partitioned handle the element interval includes the pack kernel and any halo-exchange wait. */
+int  shud_rhs_timing(shud_rhs_t h, int max_evals, int stride);
+int  shud_rhs_timing_read(shud_rhs_t h, double *ms_ele, double *ms_riv, double *ms_eval, int *n_evals);
 
 /* ---- partitioned (one process per GPU, RCCL halo) API, SURVEY §8e ----
  * Local numbering: elements [owned | seg-ghost | ghost], reaches [owned | ghost]; segments are

@@ -67,8 +67,17 @@ enum ClassField {
     CF_r_fcmr, CF_r_dTh, CF_r_infD, CF_r_Sy,
     CF_COUNT
 };
+// record stride of the class table (8-B words), odd: lanes reading one field of different classes from the
+// LDS copy land on different banks (an even stride of 32 put every class on one bank)
+constexpr int CF_STRIDE = CF_COUNT | 1;
+// most classes one workgroup stages in LDS (128 x 33 x 8 B = 33 KiB)
+#ifndef SHUD_LDS_CLS_MAX
+#define SHUD_LDS_CLS_MAX 128
+#endif
+constexpr int kLdsClassMax = SHUD_LDS_CLS_MAX;
+
 struct DevPacked {
-    const double *ctab;     // [CF_COUNT][ncls]
+    const double *ctab;     // [ncls][CF_STRIDE] record-major: one class's fields share 2-3 cache lines
     int ncls;
     const double2 *zz;      // {z_surf, z_bottom}  (aquifer_depth == z_surf - z_bottom, checked at create)
     const int4 *meta;       // {nabr0, nabr1, nabr2, cf}: cf bits 0-7 iBC (int8), 8-9 iSS class,

@@ -67,13 +67,8 @@ __device__ __forceinline__ double ugw_pk(const DevMesh &m, double ygw_raw, int i
 
 // class table staged in LDS (record-major [class][field]) when it has <= LDS_CLS_MAX classes: the 18 + 3x5
 // class lookups per element become LDS reads with immediate offsets instead of dependent L2 trips
-#ifndef SHUD_LDS_CLS_MAX
-#define SHUD_LDS_CLS_MAX 128
-#endif
-constexpr int LDS_CLS_MAX = SHUD_LDS_CLS_MAX;
-// odd record stride (in 8-B words): lanes of one wave reading the same field of different classes land on
-// different LDS banks (an even stride of 32 words put every class on one bank: ~960 conflict cycles/wave)
-constexpr int CF_LDS_STRIDE = CF_COUNT | 1;
+constexpr int LDS_CLS_MAX = kLdsClassMax;
+constexpr int CF_LDS_STRIDE = CF_STRIDE;   // the HBM table's record layout, copied linearly into LDS
 
 // LAKE: the model has lakes.  Lake elements (cf bit 31) follow updateLakeElement /
 // fun_Ele_lakeVertical / fun_Ele_lakeHorizon (Element.cpp:336-346, MD_ElementFlux.cpp:2-23) and get zero DY
@@ -89,10 +84,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     extern __shared__ double lct[];                       // ncls * CF_LDS_STRIDE doubles when LCT
     const int ncls = p.ncls;
     if (LCT) {
-        for (int t = threadIdx.x; t < ncls * CF_COUNT; t += blockDim.x) {
-            const int c = t / CF_COUNT, f = t - c * CF_COUNT;
-            lct[c * CF_LDS_STRIDE + f] = p.ctab[f * ncls + c];
-        }
+        for (int t = threadIdx.x; t < ncls * CF_LDS_STRIDE; t += blockDim.x) lct[t] = p.ctab[t];
         __syncthreads();
     }
     const int i = i0 + block_id<1>() * blockDim.x + threadIdx.x;   // elements [i0, n_compute)
@@ -113,7 +105,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     double2 fu;
     if (FU1) { fu.x = 1.0; fu.y = 1.0; } else fu = ldnt2(&p.s_fu[i]);
     const double2 csv = ldnt2(&p.cs[cur][i]);
-#define CL(f) (LCT ? lct[cid * CF_LDS_STRIDE + CF_##f] : p.ctab[CF_##f * ncls + cid])
+#define CL(f) (LCT ? lct[cid * CF_LDS_STRIDE + CF_##f] : p.ctab[cid * CF_STRIDE + CF_##f])
 #define CDIV(a, F) CDIV_(a, CL(F), CL(r_##F))
 
     // ---- f_update ----
@@ -267,7 +259,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         const double B = g.x, d2n = g.y;
         double qsf = 0., qsb = 0.;
         const int cn = cf_class(ncf);
-#define CN(f) (LCT ? lct[cn * CF_LDS_STRIDE + CF_##f] : p.ctab[CF_##f * ncls + cn])
+#define CN(f) (LCT ? lct[cn * CF_LDS_STRIDE + CF_##f] : p.ctab[cn * CF_STRIDE + CF_##f])
         if (LAKE && nb >= 0 && ncf < 0) {                 // bank edge: the neighbour is a lake element
             const int l = lk.lake_of[nb];
             const double zl = lk.bathy_y[lk.bathy_off[l]];               // lake[l].zmin = bathymetry.yi[0]

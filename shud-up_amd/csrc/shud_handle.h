@@ -89,6 +89,11 @@ struct shud_rhs {
     ncclComm_t comm = nullptr;
     hipStream_t s_comm = nullptr;        // RCCL halo exchange, overlapped with the interior element kernel
     hipEvent_t ev_pack = nullptr, ev_comm = nullptr;
+    // in-loop kernel timing (shud_rhs_timing): 3 events per device eval {start, after element kernel(s),
+    // after river (+lake) kernel}, recorded on the handle's stream while enabled
+    int tm_cap = 0, tm_n = 0, tm_stride = 1;
+    long long tm_seen = 0;
+    std::vector<hipEvent_t> tm_ev;
     std::vector<int> esend_off, erecv_off, rsend_off, rrecv_off;
     int *d_esend_idx = nullptr, *d_rsend_idx = nullptr;
     int n_esend = 0, n_rsend = 0, n_eghost = 0, n_rghost = 0;

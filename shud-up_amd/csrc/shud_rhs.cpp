@@ -359,7 +359,12 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         cls[i] = it->second;
     }
     const int ncls = (int)table.size();
-    std::vector<double> ctab((size_t)CF_COUNT * ncls);
+    // beyond what one workgroup's LDS copy holds, the class lookups become dependent L2 trips: measured on
+    // syn-10M with 13,200 classes, 1.47 ms per element kernel against 1.05 ms for the SoA kernel
+    // (bench.py many_class) -> SoA, unless SHUD_RHS_L2_CLASS=1 asks for the L2 table (A/B, bench)
+    const char *l2 = getenv("SHUD_RHS_L2_CLASS");
+    if (ncls > kLdsClassMax && !(l2 && l2[0] == '1')) return 0;
+    std::vector<double> ctab((size_t)CF_STRIDE * ncls, 0.0);
     for (int c = 0; c < ncls; c++) {
         std::vector<double> &t = table[c];
         t.resize(CF_COUNT);
@@ -381,7 +386,7 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         t[CF_r_dTh] = 1. / t[CF_dTh];
         t[CF_r_infD] = 1. / t[CF_infD];
         t[CF_r_Sy] = 1. / t[CF_Sy];
-        for (int f = 0; f < CF_COUNT; f++) ctab[(size_t)f * ncls + c] = t[f];
+        for (int f = 0; f < CF_COUNT; f++) ctab[(size_t)c * CF_STRIDE + f] = t[f];
     }
     std::vector<double2> zz(NE), ged(3 * (size_t)NE);
     std::vector<int4> meta(NE);
@@ -595,6 +600,7 @@ static void destroy_handle(shud_rhs *h) {
     shud_et_free(h);
     if (h->ev_pack) (void)hipEventDestroy(h->ev_pack);
     if (h->ev_comm) (void)hipEventDestroy(h->ev_comm);
+    for (auto e : h->tm_ev) (void)hipEventDestroy(e);
     if (h->s_comm) (void)hipStreamDestroy(h->s_comm);
     for (void *p : h->allocs) (void)hipFree(p);
     if (h->h_err) (void)hipHostFree(h->h_err);
@@ -760,15 +766,18 @@ static const uint32_t kFatal = SHUD_EF_NAN_QELE | SHUD_EF_EFFKH | SHUD_EF_ET_NEG
 
 // partitioned handles: the interior elements [0, n_int) run while the halo exchange is in flight (RCCL on
 // s_comm); boundary + ghost elements and the reaches wait for it.  Unpartitioned: one launch each.
-static int launch_split(shud_rhs *h, const double *y, double *dy) {
+static int launch_split(shud_rhs *h, const double *y, double *dy, hipEvent_t e_mid = nullptr) {
     if (h->partitioned && h->packed && !h->variant && h->n_int > 0) {
         launch_ele(h, y, dy, h->cur, h->cur_e, false, 0, h->n_int);
         if (h->use_nccl) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_comm, 0));
         launch_ele(h, y, dy, h->cur, h->cur_e, false, h->n_int, h->n_own + h->n_segghost);
+        if (e_mid) HIP_TRY(hipEventRecord(e_mid, h->stream));
         launch_riv(h, y, dy, false);
     } else {
         if (h->use_nccl) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_comm, 0));
-        launch_all(h, y, dy, h->cur, h->cur_e, false);
+        launch_ele(h, y, dy, h->cur, h->cur_e, false);
+        if (e_mid) HIP_TRY(hipEventRecord(e_mid, h->stream));
+        launch_riv(h, y, dy, false);
     }
     HIP_TRY(hipGetLastError());
     return 0;
@@ -776,11 +785,15 @@ static int launch_split(shud_rhs *h, const double *y, double *dy) {
 
 static int eval_device(shud_rhs *h, double t, const double *y, double *dy) {
     (void)t;
+    hipEvent_t *E = nullptr;
+    if (h->tm_n < h->tm_cap && (h->tm_seen++ % h->tm_stride) == 0) E = &h->tm_ev[3 * (size_t)h->tm_n++];
+    if (E) HIP_TRY(hipEventRecord(E[0], h->stream));
     int rc = exchange(h, y);
     if (rc) return rc;
     h->last_cur = h->cur;
     h->last_cur_e = h->cur_e;
-    if ((rc = launch_split(h, y, dy))) return rc;
+    if ((rc = launch_split(h, y, dy, E ? E[1] : nullptr))) return rc;
+    if (E) HIP_TRY(hipEventRecord(E[2], h->stream));
     flip(h);
     h->last_y = y;
     h->have_last = true;
@@ -1023,6 +1036,46 @@ extern "C" int shud_rhs_eval_compute(shud_rhs_t h, double t, const double *d_y, 
     h->last_y = d_y;
     h->have_last = true;
     h->ncalls++;
+    return SHUD_OK;
+}
+
+extern "C" int shud_rhs_timing(shud_rhs_t h, int max_evals, int stride) {
+    if (!h || max_evals < 0 || stride < 1) return shud_fail(SHUD_ERR_ARG, "bad argument");
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    const size_t need = 3 * (size_t)max_evals;
+    while (h->tm_ev.size() < need) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreate(&e));
+        h->tm_ev.push_back(e);
+    }
+    h->tm_cap = max_evals;
+    h->tm_n = 0;
+    h->tm_seen = 0;
+    h->tm_stride = stride;
+    return SHUD_OK;
+}
+
+extern "C" int shud_rhs_timing_read(shud_rhs_t h, double *ms_ele, double *ms_riv, double *ms_eval, int *n_evals) {
+    if (!h) return shud_fail(SHUD_ERR_ARG, "null handle");
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    double a = 0., b = 0., c = 0.;
+    for (int r = 0; r < h->tm_n; r++) {
+        hipEvent_t *E = &h->tm_ev[3 * (size_t)r];
+        float x = 0.f, y = 0.f, z = 0.f;
+        HIP_TRY(hipEventElapsedTime(&x, E[0], E[1]));
+        HIP_TRY(hipEventElapsedTime(&y, E[1], E[2]));
+        HIP_TRY(hipEventElapsedTime(&z, E[0], E[2]));
+        a += x; b += y; c += z;
+    }
+    const int n = h->tm_n;
+    if (ms_ele) *ms_ele = n ? a / n : 0.;
+    if (ms_riv) *ms_riv = n ? b / n : 0.;
+    if (ms_eval) *ms_eval = n ? c / n : 0.;
+    if (n_evals) *n_evals = n;
+    h->tm_n = 0;
+    h->tm_cap = 0;
     return SHUD_OK;
 }
 

@@ -178,6 +178,8 @@ FUNCTIONS = {
     "shud_rhs_stream": (C.c_void_p, [_H]),
     "shud_rhs_time_kernels": (C.c_int, [_H, C.c_double, C.c_void_p, C.c_void_p, C.c_int, c_double_p, c_double_p,
                                         C.POINTER(C.c_int), C.c_char_p, C.c_int]),
+    "shud_rhs_timing": (C.c_int, [_H, C.c_int, C.c_int]),
+    "shud_rhs_timing_read": (C.c_int, [_H, c_double_p, c_double_p, c_double_p, C.POINTER(C.c_int)]),
     "shud_rhs_nccl_unique_id": (C.c_int, [C.c_char_p]),
     "shud_rhs_create_partitioned": (C.c_int, [C.POINTER(ShudMeshSoA), C.POINTER(ShudParamsSoA),
                                               C.POINTER(ShudRhsOptions), C.POINTER(ShudPartition),

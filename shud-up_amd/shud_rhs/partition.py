@@ -277,3 +277,209 @@ def pack_send(y_owned, part):
     ebuf = np.stack([y_owned[i], y_owned[no + i], y_owned[2 * no + i]], 1).reshape(-1)
     rbuf = y_owned[3 * no + np.asarray(part.riv_send_idx, dtype=np.int64)]
     return ebuf, rbuf
+
+
+# ---------------------------------------------------------------------------------------------------------
+# The C++ partitioner and planner (include/shud_partition.h, libshud_host.so).  The functions above are the
+# Python restatement the tests cross-check it against; bench.py's N > 1 path uses the C++ ones.
+# ---------------------------------------------------------------------------------------------------------
+PART_MULTILEVEL, PART_RCB, PART_AUTO = 0, 1, 2
+
+
+class ShudPartStats(C.Structure):
+    _fields_ = [("edge_cut", C.c_int64), ("segment_cut", C.c_int64), ("graph_cut", C.c_int64),
+                ("imbalance", C.c_double), ("levels", C.c_int32), ("coarse_vertices", C.c_int32),
+                ("seconds", C.c_double), ("max_halo", C.c_int64), ("method_used", C.c_int32)]
+
+
+class ShudPlanInfo(C.Structure):
+    _fields_ = [("n_own_ele", C.c_int32), ("n_int_ele", C.c_int32), ("n_ghost_ele", C.c_int32),
+                ("n_own_riv", C.c_int32), ("n_ghost_riv", C.c_int32), ("n_seg", C.c_int32),
+                ("ele_gid", C.POINTER(C.c_int32)), ("riv_gid", C.POINTER(C.c_int32)),
+                ("seg_gid", C.POINTER(C.c_int32)), ("riv_part", C.POINTER(C.c_int32))]
+
+
+_HL = None
+
+
+def _host():
+    global _HL
+    if _HL is None:
+        from . import host
+        L = host.lib()
+        H = C.c_void_p
+        sig = {
+            "shud_partition_mesh": (C.c_int, [C.POINTER(abi.ShudMeshSoA), C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
+                                              C.c_uint64, C.c_void_p, C.POINTER(ShudPartStats)]),
+            "shud_partition_cut": (C.c_int, [C.POINTER(abi.ShudMeshSoA), C.c_void_p, C.c_int32,
+                                             C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+            "shud_partition_halo": (C.c_int, [C.POINTER(abi.ShudMeshSoA), C.c_void_p, C.c_int32, C.c_void_p,
+                                              C.c_void_p]),
+            "shud_plan_build": (C.c_int, [C.POINTER(abi.ShudMeshSoA), C.c_void_p, C.c_int32, C.c_int32,
+                                          C.POINTER(H)]),
+            "shud_plan_free": (None, [H]),
+            "shud_plan_info": (C.c_int, [H, C.POINTER(ShudPlanInfo)]),
+            "shud_plan_partition": (C.c_int, [H, C.POINTER(abi.ShudPartition)]),
+            "shud_plan_local_mesh": (C.c_int, [H, C.POINTER(abi.ShudMeshSoA), C.POINTER(abi.ShudParamsSoA),
+                                               C.POINTER(abi.ShudMeshSoA), C.POINTER(abi.ShudParamsSoA)]),
+            "shud_plan_gather_ele": (C.c_int, [H, C.c_void_p, C.c_void_p]),
+            "shud_plan_owned_state": (C.c_int, [H, C.c_void_p, C.c_int32, C.c_void_p]),
+            "shud_plan_scatter_owned": (C.c_int, [H, C.c_void_p, C.c_int32, C.c_void_p]),
+            "shud_partition_error": (C.c_char_p, []),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype, f.argtypes = res, args
+        _HL = L
+    return _HL
+
+
+def _hcheck(rc, what):
+    if rc:
+        raise RuntimeError(f"{what} failed ({rc}): {_host().shud_partition_error().decode()}")
+
+
+def cpp_partition(m, nparts, method=PART_MULTILEVEL, seed=12345):
+    """C++ element partition (multilevel HEM + FM/greedy refinement, or RCB) -> (ele_part, stats dict)."""
+    ms = m.mesh_struct()
+    part = np.zeros(m.num_ele, dtype=np.int32)
+    cx = cy = None
+    if method in (PART_RCB, PART_AUTO) and "x" in m.meta:
+        x, y = element_centroids(m)
+        cx, cy = np.ascontiguousarray(x, dtype=np.float64), np.ascontiguousarray(y, dtype=np.float64)
+    st = ShudPartStats()
+    _hcheck(_host().shud_partition_mesh(C.byref(ms), None if cx is None else cx.ctypes.data,
+                                        None if cy is None else cy.ctypes.data, int(nparts), int(method),
+                                        int(seed), part.ctypes.data, C.byref(st)), "shud_partition_mesh")
+    stats = {k: getattr(st, k) for k, _ in ShudPartStats._fields_}
+    return part, stats
+
+
+def cpp_edge_cut(m, ele_part):
+    ms = m.mesh_struct()
+    ep = np.ascontiguousarray(ele_part, dtype=np.int32)
+    ec, sc = C.c_int64(), C.c_int64()
+    _hcheck(_host().shud_partition_cut(C.byref(ms), ep.ctypes.data, int(ep.max()) + 1, C.byref(ec), C.byref(sc)),
+            "shud_partition_cut")
+    return ec.value, sc.value
+
+
+def cpp_halo(m, ele_part):
+    """(ghost elements, ghost reaches) per part, from the C++ planner's ownership rules"""
+    ms = m.mesh_struct()
+    ep = np.ascontiguousarray(ele_part, dtype=np.int32)
+    k = int(ep.max()) + 1
+    ge, gr = np.zeros(k, np.int64), np.zeros(k, np.int64)
+    _hcheck(_host().shud_partition_halo(C.byref(ms), ep.ctypes.data, k, ge.ctypes.data, gr.ctypes.data),
+            "shud_partition_halo")
+    return ge, gr
+
+
+class CppPlan:
+    """One rank's plan built by the C++ planner (shud_plan_build); .local_model() = the rank's ShudModel and
+    LocalPartition gathered by C++ (shud_plan_local_mesh / shud_plan_gather_ele)."""
+
+    def __init__(self, m, ele_part, nparts, rank):
+        self.m = m
+        self.nparts, self.rank = nparts, rank
+        self._ms = m.mesh_struct()
+        self._ep = np.ascontiguousarray(ele_part, dtype=np.int32)
+        h = C.c_void_p()
+        _hcheck(_host().shud_plan_build(C.byref(self._ms), self._ep.ctypes.data, int(nparts), int(rank),
+                                        C.byref(h)), "shud_plan_build")
+        self.h = h
+        info = ShudPlanInfo()
+        _hcheck(_host().shud_plan_info(h, C.byref(info)), "shud_plan_info")
+        ne, nr = info.n_own_ele + info.n_ghost_ele, info.n_own_riv + info.n_ghost_riv
+        self.n_own_ele, self.n_int_ele, self.n_own_riv = info.n_own_ele, info.n_int_ele, info.n_own_riv
+        self.ele_gid = np.ctypeslib.as_array(info.ele_gid, shape=(ne,)).copy()
+        self.riv_gid = np.ctypeslib.as_array(info.riv_gid, shape=(nr,)).copy()
+        self.seg_gid = (np.ctypeslib.as_array(info.seg_gid, shape=(info.n_seg,)).copy() if info.n_seg
+                        else np.zeros(0, np.int32))
+        self.riv_part = (np.ctypeslib.as_array(info.riv_part, shape=(m.num_riv,)).copy() if m.num_riv
+                         else np.zeros(0, np.int32))
+        sp = abi.ShudPartition()
+        _hcheck(_host().shud_plan_partition(h, C.byref(sp)), "shud_plan_partition")
+        P = nparts + 1
+
+        def arr(ptr, n):
+            return np.ctypeslib.as_array(ptr, shape=(n,)).copy() if n else np.zeros(0, np.int32)
+        self.ele_send_off = arr(sp.ele_send_off, P)
+        self.ele_recv_off = arr(sp.ele_recv_off, P)
+        self.riv_send_off = arr(sp.riv_send_off, P)
+        self.riv_recv_off = arr(sp.riv_recv_off, P)
+        self.ele_send_idx = arr(sp.ele_send_idx, int(self.ele_send_off[-1]))
+        self.riv_send_idx = arr(sp.riv_send_idx, int(self.riv_send_off[-1]))
+
+    def close(self):
+        if self.h:
+            _host().shud_plan_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def partition(self):
+        return LocalPartition(rank=self.rank, nranks=self.nparts, n_own_ele=self.n_own_ele, n_own_riv=self.n_own_riv,
+                              ele_gid=self.ele_gid, riv_gid=self.riv_gid, ele_send_off=self.ele_send_off,
+                              ele_send_idx=self.ele_send_idx, ele_recv_off=self.ele_recv_off,
+                              riv_send_off=self.riv_send_off, riv_send_idx=self.riv_send_idx,
+                              riv_recv_off=self.riv_recv_off, seg_gid=self.seg_gid)
+
+    def gather_ele(self, a):
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        out = np.empty(self.ele_gid.size)
+        _hcheck(_host().shud_plan_gather_ele(self.h, a.ctypes.data, out.ctypes.data), "shud_plan_gather_ele")
+        return out
+
+    def owned_state(self, y):
+        y = np.ascontiguousarray(y, dtype=np.float64)
+        out = np.empty(3 * self.n_own_ele + self.n_own_riv)
+        _hcheck(_host().shud_plan_owned_state(self.h, y.ctypes.data, self.m.num_ele, out.ctypes.data),
+                "shud_plan_owned_state")
+        return out
+
+    def local_model(self):
+        """(ShudModel, LocalPartition) of this rank, every array gathered by the C++ planner."""
+        m = self.m
+        lms, lps = abi.ShudMeshSoA(), abi.ShudParamsSoA()
+        gps = m.params_struct()
+        _hcheck(_host().shud_plan_local_mesh(self.h, C.byref(self._ms), C.byref(gps), C.byref(lms), C.byref(lps)),
+                "shud_plan_local_mesh")
+        NE, NR, NS = lms.num_ele, lms.num_riv, lms.num_seg
+
+        def d(ptr, n):
+            return np.ctypeslib.as_array(ptr, shape=(n,)).copy() if (ptr and n) else None
+        lm = ShudModel(NE, NR, NS, lms.close_boundary)
+        for k in ELE1:
+            v = d(getattr(lms, k), NE)
+            if v is not None:
+                lm.ele[k] = v
+        for k in ELE3:
+            v = d(getattr(lms, k), 3 * NE)
+            if v is not None:
+                lm.ele[k] = v
+        lm.nabr = d(lms.nabr, 3 * NE)
+        lm.ibc, lm.iss = d(lms.ibc, NE), d(lms.iss, NE)
+        lm.ilake = d(lms.ilake, NE)
+        for k in RIV_D:
+            v = d(getattr(lms, k), NR)
+            lm.riv[k] = v if v is not None else np.zeros(NR)
+        lm.riv_down = d(lms.riv_down, NR) if NR else np.zeros(0, np.int32)
+        lm.riv_bc = d(lms.riv_bc, NR) if NR else np.zeros(0, np.int32)
+        lm.seg_ele = d(lms.seg_ele, NS) if NS else np.zeros(0, np.int32)
+        lm.seg_riv = d(lms.seg_riv, NS) if NS else np.zeros(0, np.int32)
+        lm.seg_length = d(lms.seg_length, NS) if NS else np.zeros(0)
+        lm.seg_cwr = d(lms.seg_cwr, NS) if NS else np.zeros(0)
+        for k in abi.PARAM_NAMES:
+            lm.par[k] = d(getattr(lps, k), NE)
+        for k, v in m.step.items():
+            lm.step[k] = self.gather_ele(v)
+        lm.bc_tables = dict(m.bc_tables)
+        lm.meta["ele_gid"] = self.ele_gid
+        lm.meta["riv_gid"] = self.riv_gid
+        lm.finalize()
+        return lm, self.partition()

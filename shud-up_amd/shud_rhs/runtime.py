@@ -164,6 +164,17 @@ class RhsHandle:
         nm = names.value.decode().split(",")
         return ms_eval.value, {nm[k]: ms[k] for k in range(nk.value)}
 
+    def timing(self, max_evals, stride=1):
+        """record per-kernel HIP events in every `stride`-th of the next evals, up to `max_evals` of them
+        (shud_rhs_timing)"""
+        _check(lib().shud_rhs_timing(self.h, int(max_evals), int(stride)), "timing")
+
+    def timing_read(self):
+        """(ms_ele, ms_riv, ms_eval, n): per-eval averages of the evals recorded since timing()"""
+        a, b, c, n = C.c_double(), C.c_double(), C.c_double(), C.c_int()
+        _check(lib().shud_rhs_timing_read(self.h, C.byref(a), C.byref(b), C.byref(c), C.byref(n)), "timing_read")
+        return a.value, b.value, c.value, n.value
+
     # ---- output path (include/shud_out.h) ----
     def summary(self, d_y):
         """Model_Data::summary(udata) on the device: SHUD_ARR_Y_* from the state at d_y"""

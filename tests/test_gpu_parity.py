@@ -211,3 +211,27 @@ def test_fu_nonunit_and_packed_flags(oracle_mod):
         g.set_step_inputs(st); o.set_step_inputs(st)
         for c in range(2):
             assert_close(g.eval(0.0, y0), o.eval(0.0, y0)[0], what="fu step")
+
+
+def test_syn_10m(oracle_mod):
+    """syn-10M (BASELINE configs[4]'s mesh, the bench workload) on one GPU against the oracle at the strict
+    tolerance: serial semantics, the packed layout the bench runs, 2 successive calls (carried state)."""
+    from shud_rhs import synth
+    m = synth.synth_model(10_000_000)
+    m.step = workload.random_step_inputs(m)
+    y = workload.random_state(m)
+    _compare_sequence(m, [y], abi.SHUD_MODE_SERIAL, oracle_mod, ncalls=2, diag=False, label="syn-10M",
+                      layout="packed")
+
+
+@pytest.mark.parametrize("l2", ["0", "1"])
+def test_many_classes(oracle_mod, monkeypatch, l2):
+    """Per-element calibrated parameters: > 128 distinct parameter tuples.  Default: the SoA kernel; with
+    SHUD_RHS_L2_CLASS=1 the packed kernel reading its class table from L2 (record-major, no LDS copy)."""
+    monkeypatch.setenv("SHUD_RHS_L2_CLASS", l2)
+    m, y = cases.variant(20000, seed=17)
+    m.par["KsatH"] = m.par["KsatH"] * (1.0 + 1e-7 * (np.arange(m.num_ele) % 300))
+    m.par["Sy"] = m.par["Sy"] * (1.0 + 1e-9 * (np.arange(m.num_ele) % 7))
+    for mode in (abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP):
+        _compare_sequence(m, [y] + cases.states(m, None, 1, seed=3), mode, oracle_mod, ncalls=2,
+                          label=f"many-class l2={l2}", layout="packed" if l2 == "1" else "soa")

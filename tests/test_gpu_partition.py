@@ -1,7 +1,13 @@
 """GPU: partitioned handles (owned + ghost entities) on one MI355X, halo moved between the
 handles' device buffers by the test (external transport: shud_rhs_eval_pack -> D2D copies ->
 shud_rhs_eval_compute).  Owned DY must be bit-identical to the single-GPU handle's.  The RCCL transport
-used by bench.py at N > 1 replaces only the D2D copies (grouped ncclSend/ncclRecv of the same ranges)."""
+used by bench.py at N > 1 replaces only the D2D copies (grouped ncclSend/ncclRecv of the same ranges).
+
+BASELINE configs[4] (syn-10M, 8-way partition, 8 GPUs) is exercised here as far as one GPU allows: the
+8 partitioned handles of the bench's own C++ plan (include/shud_partition.h) live on one device and trade
+their halos by D2D copies; every rank's owned DY equals the unpartitioned handle's bit for bit."""
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -11,28 +17,24 @@ from shud_rhs import partition, workload
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("nranks", [2, 4])
-@pytest.mark.parametrize("mode", [0, 1])
-@pytest.mark.parametrize("packed", ["1", "0"])
-def test_partitioned_handles_bit_identical(nranks, mode, packed, monkeypatch):
-    monkeypatch.setenv("SHUD_RHS_PACKED", packed)
+def _run_ranks(m, y_list, locs, mode, ncalls=3):
+    """locs: [(local ShudModel, LocalPartition)] for every rank; compares owned DY with one unpartitioned
+    handle over `ncalls` successive stateful calls per state."""
     from shud_rhs import runtime as rt
-    m, y = cases.variant(20000, seed=17)
+    nranks = len(locs)
     single = rt.RhsHandle(m, mode=mode)
     single.set_step_inputs()
-    _, _, plans = partition.build_plans(m, nranks)
-    locs = [partition.local_model(m, plans[r], r, nranks) for r in range(nranks)]
     hs, bufs, halos = [], [], []
-    for lm, part in locs:
-        h = rt.RhsHandle(lm, mode=mode, partition=part)
-        h.set_step_inputs()
-        hs.append(h)
-        ny = 3 * part.n_own_ele + part.n_own_riv
-        bufs.append((h.device_alloc(8 * ny), h.device_alloc(8 * ny), ny))
-        halos.append(h.halo_buffers())
     try:
-        for yy in [y, workload.random_state(m, seed=2)]:
-            for call in range(3):
+        for lm, part in locs:
+            h = rt.RhsHandle(lm, mode=mode, partition=part)
+            h.set_step_inputs()
+            hs.append(h)
+            ny = 3 * part.n_own_ele + part.n_own_riv
+            bufs.append((h.device_alloc(8 * ny), h.device_alloc(8 * ny), ny))
+            halos.append(h.halo_buffers())
+        for yy in y_list:
+            for call in range(ncalls):
                 ref = single.eval(0.0, yy)
                 for r, (lm, part) in enumerate(locs):
                     hs[r].h2d(bufs[r][0], partition.local_state(yy, m, part))
@@ -47,14 +49,14 @@ def test_partitioned_handles_bit_identical(nranks, mode, packed, monkeypatch):
                         pp = locs[p][1]
                         s0, s1 = int(pp.ele_send_off[r]), int(pp.ele_send_off[r + 1])
                         d0 = int(part.ele_recv_off[p])
+                        assert s1 - s0 == int(part.ele_recv_off[p + 1]) - d0
                         if s1 > s0:
-                            import ctypes as C
                             rt.lib().shud_rhs_memcpy(hs[r].h, C.c_void_p(gele + 24 * d0), C.c_void_p(esend + 24 * s0),
                                                      24 * (s1 - s0), 3)
                         s0, s1 = int(pp.riv_send_off[r]), int(pp.riv_send_off[r + 1])
                         d0 = int(part.riv_recv_off[p])
+                        assert s1 - s0 == int(part.riv_recv_off[p + 1]) - d0
                         if s1 > s0:
-                            import ctypes as C
                             rt.lib().shud_rhs_memcpy(hs[r].h, C.c_void_p(griv + 8 * d0), C.c_void_p(rsend + 8 * s0),
                                                      8 * (s1 - s0), 3)
                 for r, (lm, part) in enumerate(locs):
@@ -67,13 +69,63 @@ def test_partitioned_handles_bit_identical(nranks, mode, packed, monkeypatch):
             h.device_free(a)
             h.device_free(b)
             h.close()
+        single.close()
+
+
+@pytest.mark.parametrize("nranks", [2, 4, 8])
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("packed", ["1", "0"])
+def test_partitioned_handles_bit_identical(nranks, mode, packed, monkeypatch):
+    """Python RCB plans (the restatement the C++ planner is checked against)."""
+    monkeypatch.setenv("SHUD_RHS_PACKED", packed)
+    m, y = cases.variant(20000, seed=17)
+    _, _, plans = partition.build_plans(m, nranks)
+    locs = [partition.local_model(m, plans[r], r, nranks) for r in range(nranks)]
+    _run_ranks(m, [y, workload.random_state(m, seed=2)], locs, mode)
+
+
+@pytest.mark.parametrize("nranks", [2, 4, 8])
+@pytest.mark.parametrize("method", [partition.PART_MULTILEVEL, partition.PART_AUTO])
+def test_cpp_plans_bit_identical(nranks, method):
+    """The C++ partitioner + planner + local-mesh gather (what bench.py N > 1 runs), serial and OMP."""
+    m, y = cases.variant(20000, seed=17)
+    ep, _ = partition.cpp_partition(m, nranks, method)
+    locs = [partition.CppPlan(m, ep, nranks, r).local_model() for r in range(nranks)]
+    for mode in (0, 1):
+        _run_ranks(m, [y, workload.random_state(m, seed=5)], locs, mode, ncalls=2)
+
+
+@pytest.mark.parametrize("nranks", [2, 8])
+def test_syn_1m_cpp_plans(nranks):
+    """syn-1M (BASELINE configs[3] mesh) split by the bench's own C++ partition into 2 and 8 ranks."""
+    from shud_rhs import synth
+    m = synth.synth_model(1_000_000)
+    m.step = workload.random_step_inputs(m)
+    ep, _ = partition.cpp_partition(m, nranks, partition.PART_AUTO)
+    locs = [partition.CppPlan(m, ep, nranks, r).local_model() for r in range(nranks)]
+    _run_ranks(m, [workload.random_state(m)], locs, 0, ncalls=2)
+
+
+def test_syn_10m_8way():
+    """BASELINE configs[4]: syn-10M in the 8-way C++ partition the bench's N = 8 run uses, 8 partitioned
+    handles on one GPU (D2D halo transport), 2 stateful calls: bit-identical to the single-GPU handle."""
+    from shud_rhs import synth
+    m = synth.synth_model(10_000_000)
+    m.step = workload.random_step_inputs(m)
+    ep, _ = partition.cpp_partition(m, 8, partition.PART_AUTO)
+    locs = []
+    for r in range(8):
+        pl = partition.CppPlan(m, ep, 8, r)
+        locs.append(pl.local_model())
+        pl.close()
+    _run_ranks(m, [workload.random_state(m)], locs, 0, ncalls=2)
 
 
 @pytest.mark.parametrize("mode", [0, 1])
 def test_rccl_comm_single_rank(mode):
     """The RCCL transport path (comm init from a unique id, comm stream + events, interior/boundary launch
     split) on a one-rank partition: must equal the unpartitioned handle bit for bit.  (N > 1 RCCL needs one
-    GPU per rank; the multi-rank data movement itself is covered by the D2D-transport test above.)"""
+    GPU per rank; the multi-rank data movement itself is covered by the D2D-transport tests above.)"""
     from shud_rhs import runtime as rt
     m, y = cases.variant(20000, seed=17)
     single = rt.RhsHandle(m, mode=mode)

@@ -3,11 +3,17 @@
 HBM bytes per launch = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024: FETCH_SIZE (KiB) reads exactly half of
 the bytes for the 4/8/16-B-per-lane coalesced reads these kernels issue on gfx950 (calibrated by
 tools/calibrate_pmc.hip, profiles/r01/pmc/calibration_*.csv; MI355X_MICROARCH.md §HBM), WRITE_SIZE is exact.
-usage: python tools/pmc_summary.py <fetch_dir> <write_dir> <num_ele> [out.json]"""
+usage: python tools/pmc_summary.py <fetch_dir> <write_dir> <num_ele> [out.json]
+The summary carries bench.kernel_src_hash() of the tree it is written from: bench.py reports `traffic` only
+while the kernel sources still hash the same (run it on the tree the passes were collected from)."""
 import csv
 import glob
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from bench import kernel_src_hash  # noqa: E402  (keys the summary to the kernel build it was measured on)
 
 
 def per_kernel(d, counter):
@@ -28,7 +34,7 @@ def main():
     fd, wd, ne = sys.argv[1], sys.argv[2], int(sys.argv[3])
     out = sys.argv[4] if len(sys.argv) > 4 else "profiles/pmc_summary.json"
     fe, wr = per_kernel(fd, "FETCH_SIZE"), per_kernel(wd, "WRITE_SIZE")
-    res = {"num_ele": ne, "method": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 calibration)", "kernels": {}}
+    res = {"num_ele": ne, "kernel_src_hash": kernel_src_hash(), "method": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 calibration)", "kernels": {}}
     for k in fe:
         rd, wb = 2 * fe[k] * 1024, wr.get(k, 0.0) * 1024
         res["kernels"][k] = {"read_bytes_per_launch": rd, "write_bytes_per_launch": wb,
