@@ -105,9 +105,13 @@ int shud_out_create(int device, void *stream, shud_out_t *out);
 int shud_out_add(shud_out_t o, const ShudPrintSpec *spec);
 /* Control_Data::ExportResults(t): every control adds its source into its buffer; controls whose interval
  * ends at t (floor(t + 0.001) % Interval == 0) write the interval mean and reset.  Sources must hold the
- * values to export (shud_rhs_summary / shud_rhs_refresh_diagnostics first), stream-ordered. */
+ * values to export (shud_rhs_summary / shud_rhs_refresh_diagnostics first), stream-ordered.  The rows of a
+ * finished interval reach the files asynchronously (copy stream + writer thread; same bytes, same order):
+ * shud_out_flush / shud_out_rows / shud_out_destroy wait for them. */
 int shud_out_export(shud_out_t o, double t);
-/* number of rows written so far by control k (tests) */
+/* wait until every exported row is written to the files (fflush'ed) */
+int shud_out_flush(shud_out_t o);
+/* number of rows written so far by control k (tests; waits for the writer) */
 int64_t shud_out_rows(shud_out_t o, int k);
 /* flushes and closes the files, frees the buffers */
 int shud_out_destroy(shud_out_t o);

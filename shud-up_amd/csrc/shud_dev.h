@@ -98,10 +98,10 @@ struct DevPacked {
     double2 *s_fu;          // {fu_surf, fu_sub}            read only when not all ones
     double2 *cs[2];         // carried {u_satn, qEleE_IC}, ping-pong
     // reaches (owned first): 16-byte records
-    const double2 *rv_a;    // {BottomWidth, bankslope}
-    const double2 *rv_b;    // {Length, BedSlope}
-    const double2 *rv_c;    // {Dist2DownStream, avgRough}
-    const double2 *rv_d;    // {depth, 0}
+    // one 64-B record per reach {BottomWidth, bankslope | Length, BedSlope | Dist2DownStream, avgRough |
+    // depth, (down, BC)}: everything a reach's own, its downstream's and its upstream reaches' QrivDown read,
+    // so a neighbour reach costs one cache line instead of one line per field pair
+    const double2 *rv;      // [4 * NR]
     const int4 *rv_i;       // {down, BC, first reach-sorted segment, #segments}
     const int4 *rv_u;       // {up0, up1, up2, #up} (ascending global order); #up = -1: use up_off/up_idx
 };

@@ -16,6 +16,7 @@
 //     contiguous chunks so the neighbour rows an element block gathers are in its own XCD's L2.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "shud_dev.h"
 #include "shud_physics.h"
@@ -357,12 +358,14 @@ struct RivP {
     double w0, bs, len, slope, d2d, n, depth;
     int down, bc;
 };
+__device__ __forceinline__ int2 rv_ib(double x) { return __builtin_bit_cast(int2, x); }   // (down, BC)
 __device__ __forceinline__ RivP riv_load(const DevPacked &p, int r) {
-    const double2 a = p.rv_a[r], b = p.rv_b[r], c = p.rv_c[r], d = p.rv_d[r];
-    const int4 ii = p.rv_i[r];
+    const double2 *q = p.rv + 4 * (size_t)r;                  // one 64-B record: a single cache line
+    const double2 a = q[0], b = q[1], c = q[2], d = q[3];
+    const int2 ib = rv_ib(d.y);
     RivP o;
     o.w0 = a.x; o.bs = a.y; o.len = b.x; o.slope = b.y; o.d2d = c.x; o.n = c.y; o.depth = d.x;
-    o.down = ii.x; o.bc = ii.y;
+    o.down = ib.x; o.bc = ib.y;
     return o;
 }
 __device__ __forceinline__ RivGeom riv_geom_p(const RivP &q, double y) { return riv_geom(q.w0, q.bs, q.len, y); }
@@ -390,7 +393,9 @@ __device__ __forceinline__ double riv_down_p(const RivP &q, double uq, const Riv
     return g.csarea * sqrt(K_GRAV * uq) * 60.;
 }
 
-template <int MODE, bool DIAG>
+// ABL (timing-only ablations, SHUD_RIV_ABL; results are wrong when != 0): bit 0 skips the upstream
+// reaches, bit 1 the segment gathers, bit 2 the downstream reach
+template <int MODE, bool DIAG, int ABL = 0>
 __global__ void __launch_bounds__(256)
 shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, DevDiag dg) {
     // XCD-chunked workgroup order: a reach's up/downstream records sit a few blocks away in index space,
@@ -398,23 +403,23 @@ shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     const int r = block_id<1>() * blockDim.x + threadIdx.x;
     if (r >= Y.n_own_riv) return;
     const RivP q = riv_load(p, r);
-    const int4 ii = p.rv_i[r];
+    const int4 ii = p.rv_i[r];                                  // {down, BC, first segment, #segments}
     const int4 up = p.rv_u[r];
     double yg;
     const double ur = riv_stage_p<MODE>(m, Y, r, q.bc, &yg);
     const RivGeom g = riv_geom_p(q, yg);
-    double qdown;
-    {
+    double qdown = 0.;
+    if (!(ABL & 4)) {
         const int d = q.down >= 0 ? q.down : r;                 // clamped: unconditional loads
-        const double2 bd = p.rv_b[d], dd = p.rv_d[d];
-        const int bcd = p.rv_i[d].y;
+        const double2 bd = p.rv[4 * (size_t)d + 1], dd = p.rv[4 * (size_t)d + 3];   // same line of d's record
+        const int bcd = rv_ib(dd.y).y;
         double ydg;
         const double ud = riv_stage_p<MODE>(m, Y, d, bcd, &ydg);
         qdown = riv_down_p(q, ur, g, ud, dd.x, bd.y);
     }
     // junction: QrivUp[down] += -QrivDown[i], i ascending (MD_f.cpp:236-240)
     double qup = 0.;
-    const int nup = up.w;
+    const int nup = (ABL & 1) ? 0 : up.w;
     if (nup >= 0) {
         const int uv[3] = {up.x, up.y, up.z};
 #pragma unroll
@@ -440,7 +445,8 @@ shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     // fluxes (scattered 8-B writes from the element kernel cost more than these gathers).  Batches of 8:
     // all index loads, then all gathers, are in flight together; the adds stay in segment order
     double qsurf = 0., qsub = 0.;
-    if (p.seg_rpos) {                            // reach-sorted fluxes: this reach's segments are contiguous
+    if (ABL & 2) {
+    } else if (p.seg_rpos) {                            // reach-sorted fluxes: this reach's segments are contiguous
         for (int k = ii.z, k1 = ii.z + ii.w; k < k1; k++) {
             const double2 q2 = p.qseg2[k];
             qsurf += q2.x;
@@ -476,6 +482,18 @@ void launch_river_kernel_packed(const DevMesh &m, const DevPacked &p, const YVie
                                 bool diag, const DevDiag &dg, hipStream_t s) {
     if (Y.n_own_riv <= 0) return;
     const dim3 grid(((Y.n_own_riv + 255) / 256 + 7) / 8 * 8), blk(256);
+    const char *abl_env = getenv("SHUD_RIV_ABL");
+    const int abl = abl_env ? atoi(abl_env) : 0;
+    if (abl && mode == 0 && !diag) {
+        switch (abl & 7) {
+        case 1: hipLaunchKernelGGL((shud_riv_kernel_packed<0, false, 1>), grid, blk, 0, s, m, p, Y, dy, dg); return;
+        case 2: hipLaunchKernelGGL((shud_riv_kernel_packed<0, false, 2>), grid, blk, 0, s, m, p, Y, dy, dg); return;
+        case 3: hipLaunchKernelGGL((shud_riv_kernel_packed<0, false, 3>), grid, blk, 0, s, m, p, Y, dy, dg); return;
+        case 4: hipLaunchKernelGGL((shud_riv_kernel_packed<0, false, 4>), grid, blk, 0, s, m, p, Y, dy, dg); return;
+        case 7: hipLaunchKernelGGL((shud_riv_kernel_packed<0, false, 7>), grid, blk, 0, s, m, p, Y, dy, dg); return;
+        default: break;
+        }
+    }
     if (mode == 0) {
         if (diag) hipLaunchKernelGGL((shud_riv_kernel_packed<0, true>), grid, blk, 0, s, m, p, Y, dy, dg);
         else hipLaunchKernelGGL((shud_riv_kernel_packed<0, false>), grid, blk, 0, s, m, p, Y, dy, dg);

@@ -7,12 +7,22 @@
 // kernel (blockIdx.y = control; a control's selected columns are a device index list when flag_IO masks some),
 // and only the controls whose interval ends scale their buffer on the device (buffer *= tau / NumUpdate, the
 // reference's expression) and come back over PCIe to be written with the reference's byte layout.
+//
+// Finished intervals leave the compute stream at once: one kernel per control writes the scaled mean into a
+// snapshot buffer and zeroes the accumulator; the snapshot goes device->host on a copy stream into one of two
+// pinned banks, and a writer thread appends the rows to the files once that copy's event has fired.  The time
+// loop only waits when both banks are still being written (the reference writes synchronously inside
+// ExportResults; the bytes written are the same, in the same order).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <deque>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "shud_handle.h"
@@ -33,9 +43,13 @@ __global__ void __launch_bounds__(256) k_accumulate(const PrintSlot *__restrict_
         s.buf[i] += s.src[s.sel ? s.sel[i] : i];                 // buffer[i] += *(PrintVar[i])
 }
 
-__global__ void __launch_bounds__(256) k_scale(double *__restrict__ buf, int n, double f) {
+// buffer[i] *= tau / NumUpdate (the reference's expression, into the snapshot), then buffer[i] = 0
+__global__ void __launch_bounds__(256) k_snap(double *__restrict__ buf, double *__restrict__ snap, int n, double f) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) buf[i] *= f;                                      // buffer[i] *= tau / NumUpdate
+    if (i < n) {
+        snap[i] = buf[i] * f;
+        buf[i] = 0.0;
+    }
 }
 
 // Model_Data::summary (MD_update.cpp:190-216): element storages and river stage from a state vector, BC
@@ -74,20 +88,83 @@ struct PrintCtrl {
     std::vector<double> icol;
     int *d_sel = nullptr;
     double *d_buf = nullptr;
-    double *h_buf = nullptr;             // pinned staging for the interval mean
+    double *d_snap = nullptr;            // the finished interval's mean, on its way to the host
+    double *h_buf[2] = {nullptr, nullptr};   // pinned banks for the interval mean
     FILE *fb = nullptr, *fa = nullptr;
     int64_t rows = 0;
 };
 
+struct OutJob {                          // one export event: rows of the controls whose interval ended
+    int bank;
+    std::vector<std::pair<int, double>> rows;   // (control, left endpoint of the interval)
+};
+
 struct shud_out {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;        // compute stream (accumulate / snapshot kernels)
+    hipStream_t s_copy = nullptr;        // device->host copies of the snapshots
+    hipEvent_t ev_snap = nullptr, ev_copied[2] = {nullptr, nullptr};
+    bool copy_pending = false;           // a snapshot copy is in flight (the next snapshot waits for it)
+    int bank = 0;
     std::vector<PrintCtrl> pc;
     std::vector<PrintSlot> slots;        // host mirror of d_slots, index-aligned with pc
     PrintSlot *d_slots = nullptr;
     int n_slots_alloc = 0;
     int max_nvar = 0;
+    // writer thread
+    std::thread writer;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<OutJob> jobs;
+    bool bank_busy[2] = {false, false};
+    bool stop = false;
+    int inflight = 0;
 };
+
+static void writer_loop(shud_out *o) {
+    (void)hipSetDevice(o->device);
+    for (;;) {
+        OutJob job;
+        {
+            std::unique_lock<std::mutex> lk(o->mu);
+            o->cv.wait(lk, [&] { return o->stop || !o->jobs.empty(); });
+            if (o->jobs.empty()) return;
+            job = std::move(o->jobs.front());
+            o->jobs.pop_front();
+        }
+        (void)hipEventSynchronize(o->ev_copied[job.bank]);
+        for (const auto &r : job.rows) {
+            PrintCtrl &p = o->pc[r.first];
+            const double tq = r.second;
+            const double *hb = p.h_buf[job.bank];
+            if (p.fa) {                                              // fun_printASCII
+                fprintf(p.fa, "%.1f\t", tq);
+                for (int i = 0; i < p.numvar; i++) fprintf(p.fa, "%e\t", hb[i]);
+                fprintf(p.fa, "\n");
+            }
+            if (p.fb) {                                              // fun_printBINARY
+                fwrite(&tq, sizeof(double), 1, p.fb);
+                fwrite(hb, sizeof(double), p.numvar, p.fb);
+            }
+        }
+        {
+            std::lock_guard<std::mutex> lk(o->mu);
+            o->bank_busy[job.bank] = false;
+            o->inflight--;
+        }
+        o->cv.notify_all();
+    }
+}
+
+// wait until every queued row is in the files (flushed to the C library)
+static void out_drain(shud_out *o) {
+    std::unique_lock<std::mutex> lk(o->mu);
+    o->cv.wait(lk, [&] { return o->inflight == 0; });
+    for (PrintCtrl &p : o->pc) {
+        if (p.fb) fflush(p.fb);
+        if (p.fa) fflush(p.fa);
+    }
+}
 
 static int out_fail_io(const char *what, const std::string &f) {
     return shud_fail(SHUD_ERR_ARG, "%s: cannot open %s", what, f.c_str());
@@ -100,6 +177,10 @@ extern "C" int shud_out_create(int device, void *stream, shud_out_t *out) {
     shud_out *o = new shud_out;
     o->device = device;
     o->stream = (hipStream_t)stream;
+    HIP_TRY(hipStreamCreateWithFlags(&o->s_copy, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&o->ev_snap, hipEventDisableTiming));
+    for (int b = 0; b < 2; b++) HIP_TRY(hipEventCreateWithFlags(&o->ev_copied[b], hipEventDisableTiming));
+    o->writer = std::thread(writer_loop, o);
     *out = o;
     return SHUD_OK;
 }
@@ -111,6 +192,7 @@ extern "C" int shud_out_add(shud_out_t o, const ShudPrintSpec *s) {
                                            s->basename);
     if (s->n_all < 0 || s->interval < 0) return shud_fail(SHUD_ERR_ARG, "bad n_all / interval");
     HIP_TRY(hipSetDevice(o->device));
+    out_drain(o);                        // the writer indexes pc: no rows in flight while it grows
     PrintCtrl p;
     p.filename = s->basename;
     p.start_time = (long long)s->start_time;
@@ -127,8 +209,9 @@ extern "C" int shud_out_add(shud_out_t o, const ShudPrintSpec *s) {
     if (p.numvar <= 0) fprintf(stderr, "WARNING: Empty columns in %s.\n;", p.filename.c_str());
     const size_t nb = std::max(p.numvar, 1);
     HIP_TRY(hipMalloc(&p.d_buf, nb * sizeof(double)));
+    HIP_TRY(hipMalloc(&p.d_snap, nb * sizeof(double)));
     HIP_TRY(hipMemsetAsync(p.d_buf, 0, nb * sizeof(double), o->stream));   // buffer[k] = 0.0
-    HIP_TRY(hipHostMalloc(&p.h_buf, nb * sizeof(double), hipHostMallocDefault));
+    for (int b = 0; b < 2; b++) HIP_TRY(hipHostMalloc(&p.h_buf[b], nb * sizeof(double), hipHostMallocDefault));
     if (s->flag_io && p.numvar < s->n_all) {
         HIP_TRY(hipMalloc(&p.d_sel, nb * sizeof(int)));
         HIP_TRY(hipMemcpy(p.d_sel, sel.data(), sel.size() * sizeof(int), hipMemcpyHostToDevice));
@@ -197,55 +280,92 @@ extern "C" int shud_out_export(shud_out_t o, double t) {
     }
     // OUTPUT_TRIGGER_EPSILON = 0.001 min (:939)
     const long long t_floor = (long long)floor(t + 0.001);
-    bool any = false;
-    for (PrintCtrl &p : o->pc) {
+    OutJob job;
+    for (size_t k = 0; k < o->pc.size(); k++) {
+        PrintCtrl &p = o->pc[k];
         p.num_update++;
         if (t_floor % p.interval != 0) continue;
-        const double f = p.tau / p.num_update;
-        if (p.numvar > 0) {
-            hipLaunchKernelGGL(k_scale, dim3((p.numvar + 255) / 256), dim3(256), 0, o->stream, p.d_buf, p.numvar, f);
-            HIP_TRY(hipMemcpyAsync(p.h_buf, p.d_buf, p.numvar * sizeof(double), hipMemcpyDeviceToHost, o->stream));
-            HIP_TRY(hipMemsetAsync(p.d_buf, 0, p.numvar * sizeof(double), o->stream));     // reset the buffer
-        }
-        any = true;
+        job.rows.emplace_back((int)k, (double)(t_floor - (long long)p.interval));  // left endpoint
     }
-    if (!any) return SHUD_OK;
-    HIP_TRY(hipStreamSynchronize(o->stream));
-    for (PrintCtrl &p : o->pc) {
-        if (t_floor % p.interval != 0) continue;
+    if (job.rows.empty()) return SHUD_OK;
+    // a free host bank (the writer may still be writing the one used two events ago)
+    const int bank = o->bank;
+    {
+        std::unique_lock<std::mutex> lk(o->mu);
+        o->cv.wait(lk, [&] { return !o->bank_busy[bank]; });
+        o->bank_busy[bank] = true;
+        o->inflight++;
+    }
+    job.bank = bank;
+    o->bank ^= 1;
+    // the snapshots are free once the previous copy has finished
+    if (o->copy_pending) HIP_TRY(hipStreamWaitEvent(o->stream, o->ev_copied[bank ^ 1], 0));
+    for (const auto &r : job.rows) {
+        PrintCtrl &p = o->pc[r.first];
+        const double f = p.tau / p.num_update;
+        if (p.numvar > 0)
+            hipLaunchKernelGGL(k_snap, dim3((p.numvar + 255) / 256), dim3(256), 0, o->stream, p.d_buf, p.d_snap,
+                               p.numvar, f);
         p.num_update = 0;
-        const double tq = (double)(t_floor - (long long)p.interval);  // left endpoint of the interval
-        if (p.fa) {                                                  // fun_printASCII
-            fprintf(p.fa, "%.1f\t", tq);
-            for (int i = 0; i < p.numvar; i++) fprintf(p.fa, "%e\t", p.h_buf[i]);
-            fprintf(p.fa, "\n");
-        }
-        if (p.fb) {                                                  // fun_printBINARY
-            fwrite(&tq, sizeof(double), 1, p.fb);
-            fwrite(p.h_buf, sizeof(double), p.numvar, p.fb);
-        }
         p.rows++;
     }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(o->ev_snap, o->stream));
+    HIP_TRY(hipStreamWaitEvent(o->s_copy, o->ev_snap, 0));
+    for (const auto &r : job.rows) {
+        PrintCtrl &p = o->pc[r.first];
+        if (p.numvar > 0)
+            HIP_TRY(hipMemcpyAsync(p.h_buf[bank], p.d_snap, p.numvar * sizeof(double), hipMemcpyDeviceToHost,
+                                   o->s_copy));
+    }
+    HIP_TRY(hipEventRecord(o->ev_copied[bank], o->s_copy));
+    o->copy_pending = true;
+    {
+        std::lock_guard<std::mutex> lk(o->mu);
+        o->jobs.push_back(std::move(job));
+    }
+    o->cv.notify_all();
+    return SHUD_OK;
+}
+
+extern "C" int shud_out_flush(shud_out_t o) {
+    if (!o) return shud_fail(SHUD_ERR_ARG, "null argument");
+    out_drain(o);
     return SHUD_OK;
 }
 
 extern "C" int64_t shud_out_rows(shud_out_t o, int k) {
     if (!o || k < 0 || k >= (int)o->pc.size()) return -1;
+    out_drain(o);
     return o->pc[k].rows;
 }
 
 extern "C" int shud_out_destroy(shud_out_t o) {
     if (!o) return SHUD_OK;
     (void)hipSetDevice(o->device);
+    out_drain(o);
+    {
+        std::lock_guard<std::mutex> lk(o->mu);
+        o->stop = true;
+    }
+    o->cv.notify_all();
+    if (o->writer.joinable()) o->writer.join();
     (void)hipStreamSynchronize(o->stream);
+    (void)hipStreamSynchronize(o->s_copy);
     for (PrintCtrl &p : o->pc) {
         if (p.fb) fclose(p.fb);
         if (p.fa) fclose(p.fa);
         if (p.d_buf) (void)hipFree(p.d_buf);
+        if (p.d_snap) (void)hipFree(p.d_snap);
         if (p.d_sel) (void)hipFree(p.d_sel);
-        if (p.h_buf) (void)hipHostFree(p.h_buf);
+        for (int b = 0; b < 2; b++)
+            if (p.h_buf[b]) (void)hipHostFree(p.h_buf[b]);
     }
     if (o->d_slots) (void)hipFree(o->d_slots);
+    if (o->ev_snap) (void)hipEventDestroy(o->ev_snap);
+    for (int b = 0; b < 2; b++)
+        if (o->ev_copied[b]) (void)hipEventDestroy(o->ev_copied[b]);
+    if (o->s_copy) (void)hipStreamDestroy(o->s_copy);
     delete o;
     return SHUD_OK;
 }

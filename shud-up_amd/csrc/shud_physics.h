@@ -43,9 +43,9 @@ namespace shud {
 // q0 = a*rb is within 1 ulp of a/b, the residual a - q0*b is exact in one fma, and one fma correction then
 // rounds to nearest exactly like IEEE division (Markstein's theorem; round-to-nearest, no under/overflow).
 // Exact, zero, infinite and NaN residuals keep q0 (signed zeros and infinities as a/b gives them).
-// SHUD_CDIV=0 uses the plain division.
+// SHUD_CDIV=0 uses the plain division (A/B: identical results, CDIV=1 measured 1 % faster on syn-10M).
 #ifndef SHUD_CDIV
-#define SHUD_CDIV 0
+#define SHUD_CDIV 1
 #endif
 __device__ __forceinline__ double cdiv(double a, double b, double rb) {
     const double q0 = a * rb;

@@ -460,16 +460,20 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         P.seg_rpos = rp_d;
         h->rseg_perm = rorder;
     }
-    std::vector<double2> ra(NR), rb(NR), rcc(NR), rd(NR);
+    std::vector<double2> rv(4 * (size_t)NR);
     std::vector<int4> ri(NR), ru(NR);
     const int nor = h->n_own_riv;
     for (int r = 0; r < NR; r++) {
-        ra[r] = make_double2(m->riv_bottom_width[r], m->riv_bankslope[r]);
-        rb[r] = make_double2(m->riv_length[r], m->riv_bed_slope[r]);
-        rcc[r] = make_double2(m->riv_dist2down[r], m->riv_avg_rough[r]);
-        rd[r] = make_double2(m->riv_depth[r], 0.0);
         const int dn = (h->lakeon && m->riv_down[r] <= -4) ? -3 : m->riv_down[r];   // into a lake: outlet formula
-        ri[r] = make_int4(dn, m->riv_bc ? m->riv_bc[r] : 0, rstart[r], rcnt[r]);
+        const int bc = m->riv_bc ? m->riv_bc[r] : 0;
+        double ib;                                                   // (down, BC) packed into the 4th slot
+        const int32_t two[2] = {dn, bc};
+        memcpy(&ib, two, sizeof ib);
+        rv[4 * (size_t)r + 0] = make_double2(m->riv_bottom_width[r], m->riv_bankslope[r]);
+        rv[4 * (size_t)r + 1] = make_double2(m->riv_length[r], m->riv_bed_slope[r]);
+        rv[4 * (size_t)r + 2] = make_double2(m->riv_dist2down[r], m->riv_avg_rough[r]);
+        rv[4 * (size_t)r + 3] = make_double2(m->riv_depth[r], ib);
+        ri[r] = make_int4(dn, bc, rstart[r], rcnt[r]);
         int4 u = make_int4(0, 0, 0, 0);
         if (r < nor) {
             const int n = up_off[r + 1] - up_off[r];
@@ -483,14 +487,11 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         }
         ru[r] = u;
     }
-    double2 *ra_d, *rb_d, *rc_d, *rd_d; int4 *ri_d, *ru_d;
-    if ((rc = h->upload(&ra_d, ra.data(), NR))) return rc;
-    if ((rc = h->upload(&rb_d, rb.data(), NR))) return rc;
-    if ((rc = h->upload(&rc_d, rcc.data(), NR))) return rc;
-    if ((rc = h->upload(&rd_d, rd.data(), NR))) return rc;
+    double2 *rv_d; int4 *ri_d, *ru_d;
+    if ((rc = h->upload(&rv_d, rv.data(), rv.size()))) return rc;
     if ((rc = h->upload(&ri_d, ri.data(), NR))) return rc;
     if ((rc = h->upload(&ru_d, ru.data(), NR))) return rc;
-    P.rv_a = ra_d; P.rv_b = rb_d; P.rv_c = rc_d; P.rv_d = rd_d; P.rv_i = ri_d; P.rv_u = ru_d;
+    P.rv = rv_d; P.rv_i = ri_d; P.rv_u = ru_d;
     h->n_classes = ncls;
     h->packed = true;
     return 0;

@@ -169,6 +169,14 @@ int main(int argc, char **argv) {
     double t = c.start_time, tnext = t;
     const long long nsteps = max_steps >= 0 && max_steps < c.num_steps ? max_steps : c.num_steps;
     int rc = 0;
+    // wall time per phase of the loop (host view: includes waiting on the device where a phase synchronizes)
+    double ph[5] = {0, 0, 0, 0, 0};         // forcing+BC rows, ET step, CVode, summary+diagnostics, export
+    auto tick = std::chrono::steady_clock::now();
+    auto lap = [&](int k) {
+        const auto now = std::chrono::steady_clock::now();
+        ph[k] += std::chrono::duration<double>(now - tick).count();
+        tick = now;
+    };
     for (long long i = 0; i < nsteps && !rc; i++) {
         tnext += c.solver_step;
         while (t + kZero < tnext) {
@@ -185,6 +193,7 @@ int main(int argc, char **argv) {
                 rc = 1;
                 break;
             }
+            lap(0);
             if (shud_et_step(h, &f)) {
                 ShudErr e;
                 shud_rhs_get_error(h, &e);
@@ -192,6 +201,7 @@ int main(int argc, char **argv) {
                 rc = e.exit_code ? e.exit_code : 1;
                 break;
             }
+            lap(1);
             if (et_sub) shud_ode_set_stop_time(ode, tout);
             const int flag = shud_ode_solve(ode, tout, d_y, SHUD_WHERE_DEVICE, &t, SHUD_ODE_NORMAL);
             if (flag < 0) {
@@ -207,14 +217,17 @@ int main(int argc, char **argv) {
                 }
                 break;
             }
+            lap(2);
         }
         if (rc) break;
         shud_rhs_summary(h, d_y);                 // Model_Data::summary(udata)
         shud_rhs_refresh_diagnostics(h);          // the flux arrays of CVODE's last f() call
+        lap(3);
         if (shud_out_export(out, t)) {            // Control_Data::ExportResults(t)
             fprintf(stderr, "shud_out_export: %s\n", shud_rhs_last_error_string());
             rc = 1;
         }
+        lap(4);
         if (!quiet && c.verbose) printf("step %lld  t = %.3f min\n", i + 1, t);
     }
     shud_rhs_synchronize(h);
@@ -231,9 +244,10 @@ int main(int argc, char **argv) {
     // one machine-readable line (tools/e2e.sh)
     printf("{\"shud_gpu\": {\"num_ele\": %d, \"t_end_min\": %.6f, \"solver_steps\": %lld, \"cvode_steps\": %lld, "
            "\"rhs_evals\": %lld, \"newton_iters\": %lld, \"krylov_iters\": %lld, \"outputs\": %d, "
-           "\"wall_s\": %.4f, \"loop_s\": %.4f, \"exit\": %d}}\n",
+           "\"wall_s\": %.4f, \"loop_s\": %.4f, \"loop_phases_s\": {\"forcing\": %.4f, \"et_step\": %.4f, "
+           "\"cvode\": %.4f, \"summary_diag\": %.4f, \"export\": %.4f}, \"host_syncs\": %lld, \"exit\": %d}}\n",
            mesh.num_ele, t, nsteps, (long long)st.nst, (long long)(st.nfe + st.nfe_ls), (long long)st.nni,
-           (long long)st.nli, nprint, wall, loop_s, rc);
+           (long long)st.nli, nprint, wall, loop_s, ph[0], ph[1], ph[2], ph[3], ph[4], (long long)st.n_sync, rc);
     shud_ode_destroy(ode);
     shud_rhs_device_free(h, d_y);
     shud_rhs_destroy(h);

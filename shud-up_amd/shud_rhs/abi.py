@@ -236,6 +236,7 @@ OUT_FUNCTIONS = {
     "shud_out_add": (C.c_int, [_H, C.POINTER(ShudPrintSpec)]),
     "shud_out_export": (C.c_int, [_H, C.c_double]),
     "shud_out_rows": (C.c_int64, [_H, C.c_int]),
+    "shud_out_flush": (C.c_int, [_H]),
     "shud_out_destroy": (C.c_int, [_H]),
 }
 

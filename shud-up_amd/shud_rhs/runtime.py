@@ -333,6 +333,10 @@ class Output:
     def rows(self, k):
         return lib().shud_out_rows(self.h, int(k))
 
+    def flush(self):
+        """wait until every exported row is in the files (shud_out_flush)"""
+        _check(lib().shud_out_flush(self.h), "shud_out_flush")
+
     def close(self):
         if self.h:
             lib().shud_out_destroy(self.h)

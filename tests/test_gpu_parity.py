@@ -47,7 +47,10 @@ def _compare_sequence(m, ys, mode, oracle_mod, ncalls=3, diag=True, label="", la
         for k in abi.FLUXOUT_ORDER:
             if mode == abi.SHUD_MODE_OMP and k in ("q_es", "q_eu", "q_eg", "q_tu", "q_tg", "q_eta", "i_beta"):
                 continue
-            assert_close(dg[k], do[k], what=f"{label} diag {k}")
+            # the *_tot / qe2r / qriv sums are near-cancelling sums of much larger fluxes: like DY they may
+            # carry the OCML-vs-glibc ulps of their terms (conftest.assert_close `blocks`, <= 0.1 % of entries)
+            sums = k in ("qele_surf_tot", "qele_sub_tot", "qe2r_surf", "qe2r_sub", "qriv_up", "qriv_surf", "qriv_sub")
+            assert_close(dg[k], do[k], what=f"{label} diag {k}", blocks=[slice(None)] if sums else None)
     assert g.num_calls() == len(ys) * ncalls
     g.close()
     return worst
