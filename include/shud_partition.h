@@ -93,6 +93,7 @@ int shud_plan_local_mesh(shud_plan_t p, const ShudMeshSoA *gmesh, const ShudPara
 /* gather a per-element global array [NE] into local order [n_own_ele + n_ghost_ele] (step inputs, carried
  * state, ET statics: ghosts carry replicated values) */
 int shud_plan_gather_ele(shud_plan_t p, const double *global, double *local);
+int shud_plan_gather_ele_i32(shud_plan_t p, const int32_t *global, int32_t *local);
 /* owned block of a global state vector: [sf|us|gw|riv](global) -> [sf|us|gw|riv](owned, local order) */
 int shud_plan_owned_state(shud_plan_t p, const double *y_global, int32_t ne_global, double *y_owned);
 /* scatter an owned block back into a global vector (tests / gathers of a distributed result) */

@@ -10,9 +10,10 @@
 //
 // Finished intervals leave the compute stream at once: one kernel per control writes the scaled mean into a
 // snapshot buffer and zeroes the accumulator; the snapshot goes device->host on a copy stream into one of two
-// pinned banks, and a writer thread appends the rows to the files once that copy's event has fired.  The time
-// loop only waits when both banks are still being written (the reference writes synchronously inside
-// ExportResults; the bytes written are the same, in the same order).
+// pinned banks, and writer threads (controls dealt round-robin, so each file keeps one writer and its row order)
+// append the rows once that copy's event has fired.  The time loop only waits when both banks are still being
+// written (the reference writes synchronously inside ExportResults; the bytes written are the same, in the
+// same order).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -94,10 +95,11 @@ struct PrintCtrl {
     int64_t rows = 0;
 };
 
-struct OutJob {                          // one export event: rows of the controls whose interval ended
-    int bank;
-    std::vector<std::pair<int, double>> rows;   // (control, left endpoint of the interval)
+struct OutTask {                         // one row of one control: (bank, control, left endpoint of the interval)
+    int bank, ctrl;
+    double tq;
 };
+constexpr int kWriters = 4;
 
 struct shud_out {
     int device = 0;
@@ -111,46 +113,41 @@ struct shud_out {
     PrintSlot *d_slots = nullptr;
     int n_slots_alloc = 0;
     int max_nvar = 0;
-    // writer thread
-    std::thread writer;
+    // writer threads: writer w owns the controls k with k % kWriters == w
+    std::thread writer[kWriters];
     std::mutex mu;
     std::condition_variable cv;
-    std::deque<OutJob> jobs;
-    bool bank_busy[2] = {false, false};
+    std::deque<OutTask> tasks[kWriters];
+    int bank_left[2] = {0, 0};           // rows of the bank's event not yet written
     bool stop = false;
-    int inflight = 0;
 };
 
-static void writer_loop(shud_out *o) {
+static void writer_loop(shud_out *o, int w) {
     (void)hipSetDevice(o->device);
     for (;;) {
-        OutJob job;
+        OutTask job;
         {
             std::unique_lock<std::mutex> lk(o->mu);
-            o->cv.wait(lk, [&] { return o->stop || !o->jobs.empty(); });
-            if (o->jobs.empty()) return;
-            job = std::move(o->jobs.front());
-            o->jobs.pop_front();
+            o->cv.wait(lk, [&] { return o->stop || !o->tasks[w].empty(); });
+            if (o->tasks[w].empty()) return;
+            job = o->tasks[w].front();
+            o->tasks[w].pop_front();
         }
         (void)hipEventSynchronize(o->ev_copied[job.bank]);
-        for (const auto &r : job.rows) {
-            PrintCtrl &p = o->pc[r.first];
-            const double tq = r.second;
-            const double *hb = p.h_buf[job.bank];
-            if (p.fa) {                                              // fun_printASCII
-                fprintf(p.fa, "%.1f\t", tq);
-                for (int i = 0; i < p.numvar; i++) fprintf(p.fa, "%e\t", hb[i]);
-                fprintf(p.fa, "\n");
-            }
-            if (p.fb) {                                              // fun_printBINARY
-                fwrite(&tq, sizeof(double), 1, p.fb);
-                fwrite(hb, sizeof(double), p.numvar, p.fb);
-            }
+        PrintCtrl &p = o->pc[job.ctrl];
+        const double *hb = p.h_buf[job.bank];
+        if (p.fa) {                                                  // fun_printASCII
+            fprintf(p.fa, "%.1f\t", job.tq);
+            for (int i = 0; i < p.numvar; i++) fprintf(p.fa, "%e\t", hb[i]);
+            fprintf(p.fa, "\n");
+        }
+        if (p.fb) {                                                  // fun_printBINARY
+            fwrite(&job.tq, sizeof(double), 1, p.fb);
+            fwrite(hb, sizeof(double), p.numvar, p.fb);
         }
         {
             std::lock_guard<std::mutex> lk(o->mu);
-            o->bank_busy[job.bank] = false;
-            o->inflight--;
+            o->bank_left[job.bank]--;
         }
         o->cv.notify_all();
     }
@@ -159,7 +156,7 @@ static void writer_loop(shud_out *o) {
 // wait until every queued row is in the files (flushed to the C library)
 static void out_drain(shud_out *o) {
     std::unique_lock<std::mutex> lk(o->mu);
-    o->cv.wait(lk, [&] { return o->inflight == 0; });
+    o->cv.wait(lk, [&] { return o->bank_left[0] == 0 && o->bank_left[1] == 0; });
     for (PrintCtrl &p : o->pc) {
         if (p.fb) fflush(p.fb);
         if (p.fa) fflush(p.fa);
@@ -180,7 +177,7 @@ extern "C" int shud_out_create(int device, void *stream, shud_out_t *out) {
     HIP_TRY(hipStreamCreateWithFlags(&o->s_copy, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&o->ev_snap, hipEventDisableTiming));
     for (int b = 0; b < 2; b++) HIP_TRY(hipEventCreateWithFlags(&o->ev_copied[b], hipEventDisableTiming));
-    o->writer = std::thread(writer_loop, o);
+    for (int w = 0; w < kWriters; w++) o->writer[w] = std::thread(writer_loop, o, w);
     *out = o;
     return SHUD_OK;
 }
@@ -280,28 +277,25 @@ extern "C" int shud_out_export(shud_out_t o, double t) {
     }
     // OUTPUT_TRIGGER_EPSILON = 0.001 min (:939)
     const long long t_floor = (long long)floor(t + 0.001);
-    OutJob job;
+    std::vector<OutTask> rows;
+    const int bank = o->bank;
     for (size_t k = 0; k < o->pc.size(); k++) {
         PrintCtrl &p = o->pc[k];
         p.num_update++;
         if (t_floor % p.interval != 0) continue;
-        job.rows.emplace_back((int)k, (double)(t_floor - (long long)p.interval));  // left endpoint
+        rows.push_back(OutTask{bank, (int)k, (double)(t_floor - (long long)p.interval)});   // left endpoint
     }
-    if (job.rows.empty()) return SHUD_OK;
-    // a free host bank (the writer may still be writing the one used two events ago)
-    const int bank = o->bank;
+    if (rows.empty()) return SHUD_OK;
+    // a free host bank (the writers may still be writing the one used two events ago)
     {
         std::unique_lock<std::mutex> lk(o->mu);
-        o->cv.wait(lk, [&] { return !o->bank_busy[bank]; });
-        o->bank_busy[bank] = true;
-        o->inflight++;
+        o->cv.wait(lk, [&] { return o->bank_left[bank] == 0; });
     }
-    job.bank = bank;
     o->bank ^= 1;
     // the snapshots are free once the previous copy has finished
     if (o->copy_pending) HIP_TRY(hipStreamWaitEvent(o->stream, o->ev_copied[bank ^ 1], 0));
-    for (const auto &r : job.rows) {
-        PrintCtrl &p = o->pc[r.first];
+    for (const auto &r : rows) {
+        PrintCtrl &p = o->pc[r.ctrl];
         const double f = p.tau / p.num_update;
         if (p.numvar > 0)
             hipLaunchKernelGGL(k_snap, dim3((p.numvar + 255) / 256), dim3(256), 0, o->stream, p.d_buf, p.d_snap,
@@ -312,8 +306,8 @@ extern "C" int shud_out_export(shud_out_t o, double t) {
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(o->ev_snap, o->stream));
     HIP_TRY(hipStreamWaitEvent(o->s_copy, o->ev_snap, 0));
-    for (const auto &r : job.rows) {
-        PrintCtrl &p = o->pc[r.first];
+    for (const auto &r : rows) {
+        PrintCtrl &p = o->pc[r.ctrl];
         if (p.numvar > 0)
             HIP_TRY(hipMemcpyAsync(p.h_buf[bank], p.d_snap, p.numvar * sizeof(double), hipMemcpyDeviceToHost,
                                    o->s_copy));
@@ -322,7 +316,8 @@ extern "C" int shud_out_export(shud_out_t o, double t) {
     o->copy_pending = true;
     {
         std::lock_guard<std::mutex> lk(o->mu);
-        o->jobs.push_back(std::move(job));
+        o->bank_left[bank] = (int)rows.size();
+        for (const auto &r : rows) o->tasks[r.ctrl % kWriters].push_back(r);
     }
     o->cv.notify_all();
     return SHUD_OK;
@@ -349,7 +344,8 @@ extern "C" int shud_out_destroy(shud_out_t o) {
         o->stop = true;
     }
     o->cv.notify_all();
-    if (o->writer.joinable()) o->writer.join();
+    for (int w = 0; w < kWriters; w++)
+        if (o->writer[w].joinable()) o->writer[w].join();
     (void)hipStreamSynchronize(o->stream);
     (void)hipStreamSynchronize(o->s_copy);
     for (PrintCtrl &p : o->pc) {

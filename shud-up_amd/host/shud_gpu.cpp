@@ -2,6 +2,7 @@
 // prelude, the integrator and the outputs on one MI355X, driven through the C-ABIs of include/.
 //
 //   shud_gpu [-o outdir] [-e end_day] [-n num_steps] [-C cwd] [-q] <input_dir> <project>
+//   shud_gpu --rhs-check K | --rhs-bench [--evals N] ...   partitioned RHS modes (shud_gpu_part.cpp)
 //
 // input_dir/<project>.* are the reference's input files (FileIn, IO.cpp:53-91); forcing csv paths in
 // <project>.tsd.forc resolve against -C (default: the process cwd, as the reference runs from its repository
@@ -36,8 +37,12 @@
 static constexpr double kZero = 1.0e-10;          // ZERO (Macros.hpp:32)
 
 static void usage() {
-    fprintf(stderr, "usage: shud_gpu [-o outdir] [-e end_day] [-n num_steps] [-C cwd] [-q] <input_dir> <project>\n");
+    fprintf(stderr, "usage: shud_gpu [-o outdir] [-e end_day] [-n num_steps] [-C cwd] [-q] <input_dir> <project>\n"
+                    "       shud_gpu --rhs-check K | --rhs-bench [--evals N] [-o outdir] [-C cwd] <input_dir> <project>\n");
 }
+
+int shud_gpu_rhs_partition(shud_project_t p, int nparts_check, bool bench, int nevals, const std::string &outdir,
+                           bool quiet);
 
 static int mkdirs(const std::string &d) {
     std::string cur;
@@ -58,6 +63,8 @@ int main(int argc, char **argv) {
     double end_day = -1.0;
     long long max_steps = -1;
     bool quiet = false;
+    int rhs_check = 0, evals = 0;
+    bool rhs_bench = false;
     std::vector<const char *> pos;
     for (int i = 1; i < argc; i++) {
         const std::string a = argv[i];
@@ -66,6 +73,9 @@ int main(int argc, char **argv) {
         else if (a == "-n" && i + 1 < argc) max_steps = atoll(argv[++i]);
         else if (a == "-C" && i + 1 < argc) cwd = argv[++i];
         else if (a == "-q") quiet = true;
+        else if (a == "--rhs-check" && i + 1 < argc) rhs_check = atoi(argv[++i]);
+        else if (a == "--rhs-bench") rhs_bench = true;
+        else if (a == "--evals" && i + 1 < argc) evals = atoi(argv[++i]);
         else if (a == "-h" || a == "--help") { usage(); return 0; }
         else pos.push_back(argv[i]);
     }
@@ -79,6 +89,12 @@ int main(int argc, char **argv) {
     if (shud_project_load(indir, prj, cwd.empty() ? nullptr : cwd.c_str(), end_day, &p)) {
         fprintf(stderr, "%s\n", shud_project_error());
         return 1;
+    }
+    if (rhs_check > 0 || rhs_bench) {
+        const int rc = shud_gpu_rhs_partition(p, rhs_check, rhs_bench, evals > 0 ? evals : (rhs_bench ? 100 : 6),
+                                              outdir, quiet);
+        shud_project_free(p);
+        return rc;
     }
     ShudControl c;
     shud_project_control(p, &c);

@@ -932,6 +932,12 @@ extern "C" int shud_plan_gather_ele(shud_plan_t p, const double *g, double *l) {
     return 0;
 }
 
+extern "C" int shud_plan_gather_ele_i32(shud_plan_t p, const int32_t *g, int32_t *l) {
+    if (!p || !g || !l) return perr(SHUD_ERR_ARG, "null argument");
+    for (size_t k = 0; k < p->ele_gid.size(); k++) l[k] = g[p->ele_gid[k]];
+    return 0;
+}
+
 extern "C" int shud_plan_owned_state(shud_plan_t p, const double *y, int32_t neg, double *o) {
     if (!p || !y || !o || neg != p->NEg) return perr(SHUD_ERR_ARG, "bad argument");
     const int no = p->n_own_ele, nro = p->n_own_riv;

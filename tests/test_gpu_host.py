@@ -144,3 +144,34 @@ def test_device_loop_vs_oracle_chain_first_hour(tmp_path):
         assert sd[key] == so[key], (key, sd[key], so[key])
     d.close()
     h.close()
+
+
+@pytest.mark.parametrize("parts", [2, 4, 8])
+def test_shud_gpu_rhs_partition_check(tmp_path, parts):
+    """shud_gpu --rhs-check K: the C++ host partitions a synthetic project (C++ partitioner + planner), drives K
+    partitioned RHS handles on one GPU with the halo moved by D2D copies and the ET prelude run on every local
+    mesh, and compares every owned DY with the unpartitioned handle's: zero mismatched entries (bit-identical)."""
+    import json
+    src = tmp_path / "in"
+    synth.write_project(str(src), "syn", 30000, days=1.0, max_step=10.0, et_step=60.0, dt_out=60)
+    r = subprocess.run([SHUD_GPU, "--rhs-check", str(parts), "--evals", "6", "-C", str(src), str(src), "syn"],
+                       capture_output=True, text=True, timeout=240)
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith('{"shud_gpu_rhs_check"')]
+    assert r.returncode == 0 and line, r.stdout + r.stderr
+    res = json.loads(line[-1])["shud_gpu_rhs_check"]
+    assert res["parts"] == parts and res["evals"] == 6 and res["mismatched_entries"] == 0, res
+    assert res["max_ghost_ele"] > 0 and res["imbalance"] < 1.05
+
+
+def test_shud_gpu_rhs_bench_single_rank(tmp_path):
+    """shud_gpu --rhs-bench with WORLD_SIZE = 1 (the N > 1 mode runs one process per GPU over RCCL)."""
+    import json
+    src = tmp_path / "in"
+    synth.write_project(str(src), "syn", 30000, days=1.0, max_step=10.0, et_step=60.0, dt_out=60)
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([SHUD_GPU, "--rhs-bench", "--evals", "20", "-o", str(tmp_path / "o"), "-C", str(src),
+                        str(src), "syn"], capture_output=True, text=True, timeout=240, env=env)
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith('{"shud_gpu_rhs_bench"')]
+    assert r.returncode == 0 and line, r.stdout + r.stderr
+    res = json.loads(line[-1])["shud_gpu_rhs_bench"]
+    assert res["evals"] == 20 and res["exit_code"] == 0 and res["ms_per_eval"] > 0
