@@ -34,6 +34,11 @@ def log(*a):
 
 
 def main():
+    # stdout carries exactly one JSON line: libraries that print banners on it (RCCL prints its version block
+    # at communicator init) write to stderr instead until the line is printed
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
@@ -108,6 +113,10 @@ def main():
     dy_t = torch.empty_like(y_t)
     yp, dyp = y_t.data_ptr(), dy_t.data_ptr()
 
+    # the STREAM probes (~50 ms of full-bandwidth traffic) run before the warm-up: the clock transient a cold
+    # GPU goes through in its first ~20 ms of load (element kernel 0.62 -> 0.74 -> 0.62 ms, profiles/r02/kt) then
+    # falls outside the K timed evals instead of inside a short K = 20 window
+    sp = stream_probe(local) if world == 1 else {}
     for _ in range(args.warmup):
         h.eval_device(0.0, yp, dyp)
     torch.cuda.synchronize()
@@ -192,8 +201,7 @@ def main():
         },
         "cpu_baseline": None,
     }
-    # the practical HBM ceilings on this box: STREAM copy and read-only sweeps (libshud_stream.so)
-    sp = stream_probe(local) if world == 1 else {}
+    # the practical HBM ceilings on this box (measured before the warm-up, see there)
     if sp:
         out["roofline"].update(sp)
         out["roofline"]["frac_of_stream_copy"] = achieved / 1e9 / sp["stream_copy_GBs"]
@@ -242,7 +250,8 @@ def main():
     if world > 1:
         dist.barrier()
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if h is not None:
         h.close()
     if world > 1:

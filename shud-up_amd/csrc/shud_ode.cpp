@@ -74,7 +74,9 @@ struct shud_ode {
     double *base = nullptr, *zn = nullptr, *ewt = nullptr, *y = nullptr, *acor = nullptr, *ftemp = nullptr;
     double *tempv = nullptr, *delta = nullptr, *work = nullptr, *V = nullptr;
     double *d_part = nullptr, *d_ds = nullptr, *h_ds = nullptr;
+    unsigned *d_counter = nullptr;
     Red red{};
+    Red rs(int slot) const { Red r = red; r.slot0 = slot; return r; }   // this reduction's result slots
     // SPGMR host state
     double Hes[kMaxL + 1][kMaxL]{}, gv[2 * kMaxL]{}, yg[kMaxL + 1]{};
     // integrator scalars (cvode_impl.h names)
@@ -99,12 +101,10 @@ struct shud_ode {
         if (rv != 0) hip_failed = true;
         return rv;
     }
-    // host fetch of the scalar slots (+ the RHS physics error word)
+    // host view of the scalar slots (+ the RHS physics error word): the last block of every reduction writes them
+    // into host-mapped memory (shud_ode_kernels.hip block_partial), so a fetch is one stream synchronize
     bool fetch() {
-        hipError_t e = hipMemcpyAsync(h_ds, d_ds, S_COUNT * sizeof(double), hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess && rh)
-            e = hipMemcpyAsync(h_ds + S_COUNT, &rh->d_err->flags, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        hipError_t e = hipStreamSynchronize(s);
         if (e == hipSuccess) e = hipGetLastError();
         n_sync++;
         if (e != hipSuccess) {
@@ -259,23 +259,20 @@ struct shud_ode {
         const double bnorm = wrms_of(S_RES);
         Coefs none{};
         if (bnorm <= deltar) {                                       // cvLsSolve: small rhs
-            newton_update(n, nullptr, n, 0, none, curiter > 0 ? nullptr : delta, ewt, acor, red, s);
-            finalize(red, 2, 0u, d_ds, S_DEL, s);
+            newton_update(n, nullptr, n, 0, none, curiter > 0 ? nullptr : delta, ewt, acor, rs(S_DEL), s);
             return fetch() ? 0 : -1;
         }
         const double delta_tol = deltar * nrmfac;
         const double r_norm = std::sqrt(h_ds[S_RES]), beta = r_norm;
         if (r_norm <= delta_tol) {                                   // SPGMR: x = x0 = 0
-            newton_update(n, nullptr, n, 0, none, nullptr, ewt, acor, red, s);
-            finalize(red, 2, 0u, d_ds, S_DEL, s);
+            newton_update(n, nullptr, n, 0, none, nullptr, ewt, acor, rs(S_DEL), s);
             return fetch() ? 0 : -1;
         }
         double rho = beta, rotation_product = 1.0;
         int krydim = 0, converged = 0, nl = 0;
         for (int i = 0; i <= maxl; ++i)
             for (int j = 0; j < maxl; ++j) Hes[i][j] = 0.0;
-        krylov_v0(n, delta, ewt, 1.0 / r_norm, VV(0), red, s);
-        finalize(red, 1, 0u, d_ds, S_SIG, s);
+        krylov_v0(n, delta, ewt, 1.0 / r_norm, VV(0), rs(S_SIG), s);
         int rv = LS_CONV_FAIL;
         for (int ll = 0; ll < maxl; ++ll) {
             nl++;
@@ -285,17 +282,14 @@ struct shud_ode {
             if (rhs(tn, work, VV(ll + 1)) != 0) return -1;
             nfeDQ++;
             njtimes++;
-            atimes(n, VV(ll + 1), ftemp, VV(ll), ewt, VV(0), -gamma, d_ds, red, s);
-            finalize(red, 2, 0u, d_ds, S_W, s);                    // [S_W, S_H0] = [||w||^2, V[0].w]
+            atimes(n, VV(ll + 1), ftemp, VV(ll), ewt, VV(0), -gamma, d_ds, rs(S_W), s);                    // [S_W, S_H0] = [||w||^2, V[0].w]
             // SUNModifiedGS: w -= h[i-1] V[i-1] fused with h[i] = V[i].w; last pass gives the new ||w||^2
             int hs = S_H0;                                           // slot of h[i-1]
             for (int i = 1; i <= ll; ++i) {
-                mgs(n, VV(ll + 1), VV(i - 1), d_ds, hs, VV(i), red, s);
-                finalize(red, 1, 0u, d_ds, S_H0 + i, s);
+                mgs(n, VV(ll + 1), VV(i - 1), d_ds, hs, VV(i), rs(S_H0 + i), s);
                 hs = S_H0 + i;
             }
-            mgs(n, VV(ll + 1), VV(ll), d_ds, hs, nullptr, red, s);
-            finalize(red, 1, 0u, d_ds, S_WN, s);
+            mgs(n, VV(ll + 1), VV(ll), d_ds, hs, nullptr, rs(S_WN), s);
             if (!fetch()) return -1;
             const double vk_norm = std::sqrt(h_ds[S_W]);
             double new_vk_norm = std::sqrt(h_ds[S_WN]);
@@ -304,13 +298,12 @@ struct shud_ode {
             if ((temp + new_vk_norm) == temp) {                      // reorthogonalise (rare)
                 double new_norm_2 = 0.0;
                 for (int i = 0; i <= ll; ++i) {
-                    mgs(n, VV(ll + 1), nullptr, d_ds, 0, VV(i), red, s);
-                    finalize(red, 1, 0u, d_ds, S_R0 + i, s);
+                    mgs(n, VV(ll + 1), nullptr, d_ds, 0, VV(i), rs(S_R0 + i), s);
                     if (!fetch()) return -1;
                     const double np = h_ds[S_R0 + i];
                     if (np == 0.0) continue;
                     Hes[i][ll] += np;
-                    mgs(n, VV(ll + 1), VV(i), d_ds, S_R0 + i, nullptr, red, s);   // w -= np V[i]
+                    mgs(n, VV(ll + 1), VV(i), d_ds, S_R0 + i, nullptr, rs(S_SCRATCH), s);   // w -= np V[i]
                     new_norm_2 += np * np;
                 }
                 if (new_norm_2 != 0.0) {
@@ -344,8 +337,7 @@ struct shud_ode {
             rotation_product *= gv[2 * ll + 1];
             rho = std::fabs(rotation_product * r_norm);
             if (rho <= delta_tol) { converged = 1; break; }
-            normalize(n, VV(ll + 1), 1.0 / Hes[ll + 1][ll], ewt, red, s);
-            finalize(red, 1, 0u, d_ds, S_SIG, s);
+            normalize(n, VV(ll + 1), 1.0 / Hes[ll + 1][ll], ewt, rs(S_SIG), s);
         }
         nli += nl;
         if (rv == LS_QR_FAIL) { ncfl++; return -1; }
@@ -370,8 +362,7 @@ struct shud_ode {
         if (rv == LS_RES_REDUCED && curiter != 0) return 1;
         Coefs c{};
         for (int k = 0; k < krydim; ++k) c.c[k] = yg[k];
-        newton_update(n, V, n, krydim, c, nullptr, ewt, acor, red, s);
-        finalize(red, 2, 0u, d_ds, S_DEL, s);
+        newton_update(n, V, n, krydim, c, nullptr, ewt, acor, rs(S_DEL), s);
         return fetch() ? 0 : -1;
     }
 
@@ -385,8 +376,7 @@ struct shud_ode {
         else vsum(n, Z(0), acor, y, s);
         if (rhs(tn, y, ftemp) != 0) return SHUD_ODE_RHSFUNC_FAIL;
         nfe++;
-        residual(n, Z(1), az ? nullptr : acor, ftemp, rl1, -gamma, ewt, delta, red, s);
-        finalize(red, 1, 0u, d_ds, S_RES, s);
+        residual(n, Z(1), az ? nullptr : acor, ftemp, rl1, -gamma, ewt, delta, rs(S_RES), s);
         if (!fetch()) return SHUD_ODE_RHSFUNC_FAIL;
         return 0;
     }
@@ -548,8 +538,7 @@ struct shud_ode {
         double cquot = 0.0;
         if (qp1) cquot = (tq[5] / saved_tq5) * rpower_i(h / tau[2], L);
         if (qm1 || qp1) {
-            eta_norms(n, qm1 ? Z(q) : nullptr, qp1 ? Z(qmax) : nullptr, acor, -cquot, ewt, red, s);
-            finalize(red, 2, 0u, d_ds, S_ETAQM1, s);
+            eta_norms(n, qm1 ? Z(q) : nullptr, qp1 ? Z(qmax) : nullptr, acor, -cquot, ewt, rs(S_ETAQM1), s);
             if (!fetch()) return -1;
         }
         if (qm1) {
@@ -622,8 +611,7 @@ struct shud_ode {
         return SHUD_ODE_SUCCESS;
     }
     int ewt_and_norm() {                                              // cvEwtSet + N_VWrmsNorm(zn[0])
-        ewt_set(n, Z(0), ewt, rtol, atol, red, s);
-        finalize(red, 2, 1u, d_ds, S_EWTMIN, s);
+        ewt_set(n, Z(0), ewt, rtol, atol, rs(S_EWTMIN), s);
         if (!fetch()) return -1;
         return h_ds[S_EWTMIN] <= 0.0 ? 1 : 0;
     }
@@ -775,9 +763,16 @@ static int ode_alloc(shud_ode *o, double t0, const double *y0, int where, const 
     HIP_TRY(hipMalloc(&o->d_part, (size_t)kMaxAcc * kMaxBlocks * sizeof(double)));
     HIP_TRY(hipMalloc(&o->d_ds, S_COUNT * sizeof(double)));
     HIP_TRY(hipMemsetAsync(o->d_ds, 0, S_COUNT * sizeof(double), o->s));
-    HIP_TRY(hipHostMalloc(&o->h_ds, (S_COUNT + 1) * sizeof(double)));
+    HIP_TRY(hipHostMalloc(&o->h_ds, (S_COUNT + 1) * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent));
+    memset(o->h_ds, 0, (S_COUNT + 1) * sizeof(double));
     o->red.part = o->d_part;
     o->red.nblk = grid_blocks(n);
+    HIP_TRY(hipMalloc(&o->d_counter, sizeof(unsigned)));
+    HIP_TRY(hipMemsetAsync(o->d_counter, 0, sizeof(unsigned), o->s));
+    HIP_TRY(hipHostGetDevicePointer((void **)&o->red.hds, o->h_ds, 0));
+    o->red.counter = o->d_counter;
+    o->red.ds = o->d_ds;
+    o->red.err = o->rh ? &o->rh->d_err->flags : nullptr;
     HIP_TRY(hipMemcpyAsync(o->zn, y0, n * sizeof(double),
                            where == SHUD_WHERE_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, o->s));
     HIP_TRY(hipStreamSynchronize(o->s));
@@ -789,6 +784,7 @@ static void ode_free(shud_ode *o) {
     if (o->base) (void)hipFree(o->base);
     if (o->d_part) (void)hipFree(o->d_part);
     if (o->d_ds) (void)hipFree(o->d_ds);
+    if (o->d_counter) (void)hipFree(o->d_counter);
     if (o->h_ds) (void)hipHostFree(o->h_ds);
     delete o;
 }

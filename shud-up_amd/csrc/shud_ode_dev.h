@@ -5,8 +5,10 @@
 // CVODE issues back to back (cvode.c / sunlinsol_spgmr.c / nvector_serial.c) so each pass reads every operand
 // once.  Per element the arithmetic is exactly the serial N_Vector kernel's (same operations, same order, no
 // FMA contraction: -ffp-contract=off).  Reductions (dot products, WRMS norms, min) are deterministic: a fixed
-// grid writes per-block partials in a fixed order, and a one-block finalize kernel sums them in a fixed order
-// into a device scalar slot `ds[slot]` that later kernels read directly (no host round trip) or the host fetches.
+// grid writes per-block partials in a fixed order, and the last block to arrive (agent-scope release / ticket /
+// acquire, cdna_hip_programming.md §6 Guideline 16) sums them in a fixed order into a device scalar slot
+// `ds[slot]` that later kernels read directly, and into its host-mapped twin `hds[slot]` (with the RHS error
+// word) that the host reads after a stream synchronize — no finalize launch and no copy per reduction.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -32,23 +34,28 @@ enum Slot : int {
     S_YCOR,         // sum (ycor*ewt)^2
     S_ETAQM1,       // sum (zn[q]*ewt)^2
     S_ETAQP1,       // sum (((-cquot) zn[qmax] + acor)*ewt)^2
+    S_SCRATCH,      // results nobody reads (the reorthogonalisation's w -= np V[i] pass)
     S_W = 15,       // sum w*w before Gram-Schmidt (vk_norm^2); atimes writes [S_W, S_H0]
     S_H0 = 16,      // S_H0 + i: Gram-Schmidt coefficient h[i][l] (first pass), i <= kMaxL
     S_R0 = S_H0 + kMaxL + 1,   // S_R0 + i: reorthogonalisation products
     S_COUNT = S_R0 + kMaxL + 1
 };
 
-struct Red {           // partial-sum scratch of one reduction launch
+struct Red {           // partial-sum scratch of one reduction launch and where its result goes
     double *part;      // [kMaxAcc][kMaxBlocks]
     int nblk;          // blocks of the producing grid (fixed per n)
+    unsigned *counter; // arrival ticket (0 between launches: the last block resets it)
+    double *ds;        // device scalar slots [S_COUNT]
+    double *hds;       // host-mapped twin [S_COUNT + 1]; hds[S_COUNT] carries the RHS error word
+    const uint32_t *err;   // RHS error flags (DevErr::flags) or null
+    int slot0;         // first slot of this reduction's results
 };
 
 struct Coefs {         // small host-computed coefficient arrays passed by value
     double c[kMaxL + 1];
 };
 
-// ---- launchers (hipStream_t s) ----
-void finalize(const Red &r, int nacc, unsigned minmask, double *ds, int slot0, hipStream_t s);
+// ---- launchers (hipStream_t s); every reduction writes its NACC results to slots [r.slot0, r.slot0 + NACC) ----
 
 void ewt_set(int64_t n, const double *zn0, double *ewt, double rtol, double atol, const Red &r, hipStream_t s);
 void predict(int64_t n, double *zn, int q, hipStream_t s);
