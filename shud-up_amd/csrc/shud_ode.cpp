@@ -74,7 +74,6 @@ struct shud_ode {
     double *base = nullptr, *zn = nullptr, *ewt = nullptr, *y = nullptr, *acor = nullptr, *ftemp = nullptr;
     double *tempv = nullptr, *delta = nullptr, *work = nullptr, *V = nullptr;
     double *d_part = nullptr, *d_ds = nullptr, *h_ds = nullptr;
-    unsigned *d_counter = nullptr;
     Red red{};
     Red rs(int slot) const { Red r = red; r.slot0 = slot; return r; }   // this reduction's result slots
     // SPGMR host state
@@ -101,8 +100,8 @@ struct shud_ode {
         if (rv != 0) hip_failed = true;
         return rv;
     }
-    // host view of the scalar slots (+ the RHS physics error word): the last block of every reduction writes them
-    // into host-mapped memory (shud_ode_kernels.hip block_partial), so a fetch is one stream synchronize
+    // host view of the scalar slots (+ the RHS physics error word): every finalize writes them into host-mapped
+    // memory (shud_ode_kernels.hip k_finalize), so a fetch is one stream synchronize
     bool fetch() {
         hipError_t e = hipStreamSynchronize(s);
         if (e == hipSuccess) e = hipGetLastError();
@@ -260,12 +259,14 @@ struct shud_ode {
         Coefs none{};
         if (bnorm <= deltar) {                                       // cvLsSolve: small rhs
             newton_update(n, nullptr, n, 0, none, curiter > 0 ? nullptr : delta, ewt, acor, rs(S_DEL), s);
+            finalize(rs(S_DEL), 2, 0u, s);
             return fetch() ? 0 : -1;
         }
         const double delta_tol = deltar * nrmfac;
         const double r_norm = std::sqrt(h_ds[S_RES]), beta = r_norm;
         if (r_norm <= delta_tol) {                                   // SPGMR: x = x0 = 0
             newton_update(n, nullptr, n, 0, none, nullptr, ewt, acor, rs(S_DEL), s);
+            finalize(rs(S_DEL), 2, 0u, s);
             return fetch() ? 0 : -1;
         }
         double rho = beta, rotation_product = 1.0;
@@ -273,6 +274,7 @@ struct shud_ode {
         for (int i = 0; i <= maxl; ++i)
             for (int j = 0; j < maxl; ++j) Hes[i][j] = 0.0;
         krylov_v0(n, delta, ewt, 1.0 / r_norm, VV(0), rs(S_SIG), s);
+        finalize(rs(S_SIG), 1, 0u, s);
         int rv = LS_CONV_FAIL;
         for (int ll = 0; ll < maxl; ++ll) {
             nl++;
@@ -283,13 +285,16 @@ struct shud_ode {
             nfeDQ++;
             njtimes++;
             atimes(n, VV(ll + 1), ftemp, VV(ll), ewt, VV(0), -gamma, d_ds, rs(S_W), s);                    // [S_W, S_H0] = [||w||^2, V[0].w]
+            finalize(rs(S_W), 2, 0u, s);
             // SUNModifiedGS: w -= h[i-1] V[i-1] fused with h[i] = V[i].w; last pass gives the new ||w||^2
             int hs = S_H0;                                           // slot of h[i-1]
             for (int i = 1; i <= ll; ++i) {
                 mgs(n, VV(ll + 1), VV(i - 1), d_ds, hs, VV(i), rs(S_H0 + i), s);
+                finalize(rs(S_H0 + i), 1, 0u, s);
                 hs = S_H0 + i;
             }
             mgs(n, VV(ll + 1), VV(ll), d_ds, hs, nullptr, rs(S_WN), s);
+            finalize(rs(S_WN), 1, 0u, s);
             if (!fetch()) return -1;
             const double vk_norm = std::sqrt(h_ds[S_W]);
             double new_vk_norm = std::sqrt(h_ds[S_WN]);
@@ -299,6 +304,7 @@ struct shud_ode {
                 double new_norm_2 = 0.0;
                 for (int i = 0; i <= ll; ++i) {
                     mgs(n, VV(ll + 1), nullptr, d_ds, 0, VV(i), rs(S_R0 + i), s);
+                    finalize(rs(S_R0 + i), 1, 0u, s);
                     if (!fetch()) return -1;
                     const double np = h_ds[S_R0 + i];
                     if (np == 0.0) continue;
@@ -338,6 +344,7 @@ struct shud_ode {
             rho = std::fabs(rotation_product * r_norm);
             if (rho <= delta_tol) { converged = 1; break; }
             normalize(n, VV(ll + 1), 1.0 / Hes[ll + 1][ll], ewt, rs(S_SIG), s);
+            finalize(rs(S_SIG), 1, 0u, s);
         }
         nli += nl;
         if (rv == LS_QR_FAIL) { ncfl++; return -1; }
@@ -363,6 +370,7 @@ struct shud_ode {
         Coefs c{};
         for (int k = 0; k < krydim; ++k) c.c[k] = yg[k];
         newton_update(n, V, n, krydim, c, nullptr, ewt, acor, rs(S_DEL), s);
+        finalize(rs(S_DEL), 2, 0u, s);
         return fetch() ? 0 : -1;
     }
 
@@ -377,6 +385,7 @@ struct shud_ode {
         if (rhs(tn, y, ftemp) != 0) return SHUD_ODE_RHSFUNC_FAIL;
         nfe++;
         residual(n, Z(1), az ? nullptr : acor, ftemp, rl1, -gamma, ewt, delta, rs(S_RES), s);
+        finalize(rs(S_RES), 1, 0u, s);
         if (!fetch()) return SHUD_ODE_RHSFUNC_FAIL;
         return 0;
     }
@@ -539,6 +548,7 @@ struct shud_ode {
         if (qp1) cquot = (tq[5] / saved_tq5) * rpower_i(h / tau[2], L);
         if (qm1 || qp1) {
             eta_norms(n, qm1 ? Z(q) : nullptr, qp1 ? Z(qmax) : nullptr, acor, -cquot, ewt, rs(S_ETAQM1), s);
+            finalize(rs(S_ETAQM1), 2, 0u, s);
             if (!fetch()) return -1;
         }
         if (qm1) {
@@ -612,6 +622,7 @@ struct shud_ode {
     }
     int ewt_and_norm() {                                              // cvEwtSet + N_VWrmsNorm(zn[0])
         ewt_set(n, Z(0), ewt, rtol, atol, rs(S_EWTMIN), s);
+        finalize(rs(S_EWTMIN), 2, 1u, s);
         if (!fetch()) return -1;
         return h_ds[S_EWTMIN] <= 0.0 ? 1 : 0;
     }
@@ -767,10 +778,7 @@ static int ode_alloc(shud_ode *o, double t0, const double *y0, int where, const 
     memset(o->h_ds, 0, (S_COUNT + 1) * sizeof(double));
     o->red.part = o->d_part;
     o->red.nblk = grid_blocks(n);
-    HIP_TRY(hipMalloc(&o->d_counter, sizeof(unsigned)));
-    HIP_TRY(hipMemsetAsync(o->d_counter, 0, sizeof(unsigned), o->s));
     HIP_TRY(hipHostGetDevicePointer((void **)&o->red.hds, o->h_ds, 0));
-    o->red.counter = o->d_counter;
     o->red.ds = o->d_ds;
     o->red.err = o->rh ? &o->rh->d_err->flags : nullptr;
     HIP_TRY(hipMemcpyAsync(o->zn, y0, n * sizeof(double),
@@ -784,7 +792,6 @@ static void ode_free(shud_ode *o) {
     if (o->base) (void)hipFree(o->base);
     if (o->d_part) (void)hipFree(o->d_part);
     if (o->d_ds) (void)hipFree(o->d_ds);
-    if (o->d_counter) (void)hipFree(o->d_counter);
     if (o->h_ds) (void)hipHostFree(o->h_ds);
     delete o;
 }

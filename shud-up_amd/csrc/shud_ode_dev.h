@@ -5,10 +5,9 @@
 // CVODE issues back to back (cvode.c / sunlinsol_spgmr.c / nvector_serial.c) so each pass reads every operand
 // once.  Per element the arithmetic is exactly the serial N_Vector kernel's (same operations, same order, no
 // FMA contraction: -ffp-contract=off).  Reductions (dot products, WRMS norms, min) are deterministic: a fixed
-// grid writes per-block partials in a fixed order, and the last block to arrive (agent-scope release / ticket /
-// acquire, cdna_hip_programming.md §6 Guideline 16) sums them in a fixed order into a device scalar slot
-// `ds[slot]` that later kernels read directly, and into its host-mapped twin `hds[slot]` (with the RHS error
-// word) that the host reads after a stream synchronize — no finalize launch and no copy per reduction.
+// grid writes per-block partials in a fixed order, and a one-block finalize kernel sums them in a fixed order
+// into a device scalar slot `ds[slot]` that later kernels read directly, and into its host-mapped twin
+// `hds[slot]` (with the RHS error word) that the host reads after a stream synchronize — no copy per fetch.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -44,7 +43,6 @@ enum Slot : int {
 struct Red {           // partial-sum scratch of one reduction launch and where its result goes
     double *part;      // [kMaxAcc][kMaxBlocks]
     int nblk;          // blocks of the producing grid (fixed per n)
-    unsigned *counter; // arrival ticket (0 between launches: the last block resets it)
     double *ds;        // device scalar slots [S_COUNT]
     double *hds;       // host-mapped twin [S_COUNT + 1]; hds[S_COUNT] carries the RHS error word
     const uint32_t *err;   // RHS error flags (DevErr::flags) or null
@@ -55,7 +53,9 @@ struct Coefs {         // small host-computed coefficient arrays passed by value
     double c[kMaxL + 1];
 };
 
-// ---- launchers (hipStream_t s); every reduction writes its NACC results to slots [r.slot0, r.slot0 + NACC) ----
+// ---- launchers (hipStream_t s); a reduction kernel leaves per-block partials, finalize(r, nacc, minmask) writes
+// its nacc results to slots [r.slot0, r.slot0 + nacc) ----
+void finalize(const Red &r, int nacc, unsigned minmask, hipStream_t s);
 
 void ewt_set(int64_t n, const double *zn0, double *ewt, double rtol, double atol, const Red &r, hipStream_t s);
 void predict(int64_t n, double *zn, int q, hipStream_t s);

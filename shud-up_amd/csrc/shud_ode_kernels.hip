@@ -22,14 +22,10 @@ int grid_blocks(int64_t n) {
 
 __device__ inline double comb(double a, double b, bool mn) { return mn ? fmin(a, b) : a + b; }
 
-// block partials: wave64 butterfly, then the 4 wave results in wave order (deterministic); then the last block to
-// arrive sums the nblk partials (lane-strided over blocks, wave butterfly, waves in order — the order the oracle
-// restates) into ds / hds.  Hand-off: cdna_hip_programming.md §6 Guideline 16, counter form (release fence
-// between the partial stores and the ticket, acquire fence on the last arriver before it reads the partials).
+// block partials: wave64 butterfly, then the 4 wave results in wave order (deterministic)
 template <int NACC>
 __device__ inline void block_partial(double (&v)[NACC], unsigned minmask, const Red &r) {
     __shared__ double sm[NACC][kThreads / 64];
-    __shared__ int last;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
     for (int a = 0; a < NACC; ++a) {
@@ -48,49 +44,41 @@ __device__ inline void block_partial(double (&v)[NACC], unsigned minmask, const 
             for (int w = 1; w < kThreads / 64; ++w) s = comb(s, sm[a][w], mn);
             r.part[(int64_t)a * kMaxBlocks + blockIdx.x] = s;
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned t = __hip_atomic_fetch_add(r.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = (t == gridDim.x - 1);
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
     }
-    __syncthreads();
-    if (!last) return;
-    const int nblk = gridDim.x;
-    double fin[NACC];
-#pragma unroll
-    for (int a = 0; a < NACC; ++a) {
+}
+
+// the nblk partials of one reduction in a fixed order (lane-strided over blocks, wave butterfly, waves in order —
+// the order the oracle restates) into the device slot ds[slot0 + a] (read by later kernels) and its host-mapped
+// twin hds[slot0 + a]; hds[S_COUNT] receives the RHS error word, so a host fetch is one stream synchronize.
+// (Finalizing in the producer's last-arriving block instead measured slower: 2048 tickets on one counter.)
+__global__ void __launch_bounds__(kThreads) k_finalize(Red r, int nacc, unsigned minmask) {
+    __shared__ double sm[kThreads / 64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int a = 0; a < nacc; ++a) {
         const bool mn = (minmask >> a) & 1u;
         double x = mn ? INFINITY : 0.0;
-        for (int b = threadIdx.x; b < nblk; b += kThreads) x = comb(x, r.part[(int64_t)a * kMaxBlocks + b], mn);
+        for (int b = threadIdx.x; b < r.nblk; b += kThreads) x = comb(x, r.part[(int64_t)a * kMaxBlocks + b], mn);
         for (int off = 32; off >= 1; off >>= 1) x = comb(x, __shfl_xor(x, off, 64), mn);
-        fin[a] = x;
-    }
-#pragma unroll
-    for (int a = 0; a < NACC; ++a)
-        if (lane == 0) sm[a][wid] = fin[a];           // sm's block partials were consumed before the barrier
-    __syncthreads();
-    if (threadIdx.x == 0) {
-#pragma unroll
-        for (int a = 0; a < NACC; ++a) {
-            const bool mn = (minmask >> a) & 1u;
-            double s = sm[a][0];
-            for (int w = 1; w < kThreads / 64; ++w) s = comb(s, sm[a][w], mn);
+        if (lane == 0) sm[wid] = x;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double s = sm[0];
+            for (int w = 1; w < kThreads / 64; ++w) s = comb(s, sm[w], mn);
             r.ds[r.slot0 + a] = s;
             r.hds[r.slot0 + a] = s;
         }
-        if (r.err) {
-            const uint32_t fl = __hip_atomic_load(r.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            double w = 0.0;
-            __builtin_memcpy(&w, &fl, sizeof(fl));
-            r.hds[S_COUNT] = w;
-        }
-        __hip_atomic_store(r.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
     }
+    if (threadIdx.x == 0 && r.err) {
+        const uint32_t fl = *(const volatile uint32_t *)r.err;
+        double w = 0.0;
+        __builtin_memcpy(&w, &fl, sizeof(fl));
+        r.hds[S_COUNT] = w;
+    }
+}
+
+void finalize(const Red &r, int nacc, unsigned minmask, hipStream_t s) {
+    k_finalize<<<1, kThreads, 0, s>>>(r, nacc, minmask);
 }
 
 // cvEwtSetSS + the N_VWrmsNorm(zn[0], ewt) of CVode's "too much accuracy" check.  24 B/entry.

@@ -15,10 +15,13 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <numeric>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -125,11 +128,20 @@ Graph dual_graph(const ShudMeshSoA *m) {
 // heavy-edge matching + contraction; returns false when the graph no longer shrinks
 bool coarsen(const Graph &g, std::mt19937_64 &rng, int64_t maxvw, Graph &c, std::vector<int32_t> &cmap) {
     const int n = g.n;
-    std::vector<int32_t> perm(n);
-    std::iota(perm.begin(), perm.end(), 0);
-    std::shuffle(perm.begin(), perm.end(), rng);
+    // visit order: blocks of 2048 consecutive vertices in a random order (block b_k = (off + k * stride) mod nb,
+    // stride coprime to nb), vertices in index order inside a block — random enough for the matching, and the
+    // adjacency of consecutive visits stays in cache (a fully scattered order costs a miss per vertex)
+    constexpr int64_t B = 2048;
+    const uint64_t nb = (uint64_t)((n + B - 1) / B);
+    uint64_t stride = (rng() % nb) | 1;
+    while (std::gcd(stride, nb) != 1) stride += 2;
+    const uint64_t off = rng() % nb;
     std::vector<int32_t> match(n, -1);
-    for (int v : perm) {
+    for (int64_t k = 0; k < (int64_t)nb * B; k++) {
+        const int64_t blk = (int64_t)((off + (uint64_t)(k / B) * stride) % nb);
+        const int64_t v64 = blk * B + k % B;
+        if (v64 >= n) continue;
+        const int v = (int)v64;
         if (match[v] >= 0) continue;
         int best = -1, bw = -1;
         for (int64_t k = g.xadj[v]; k < g.xadj[v + 1]; k++) {
@@ -337,8 +349,8 @@ void ml_bisect(const Graph &g, double f0, double ub, std::mt19937_64 &rng, std::
         cm.push_back(std::move(cmap));
         cur = &lv.back();
     }
-    if (levels) *levels = std::max(*levels, (int)lv.size());
-    if (coarse_n) *coarse_n = std::max(*coarse_n, cur->n);
+    *levels = (int)lv.size();
+    *coarse_n = cur->n;
     const int64_t t0 = (int64_t)((double)g.tvw * f0);
     const int64_t cap0 = (int64_t)std::ceil(ub * (double)g.tvw * f0);
     const int64_t cap1 = (int64_t)std::ceil(ub * (double)g.tvw * (1. - f0));
@@ -365,10 +377,15 @@ void ml_bisect(const Graph &g, double f0, double ub, std::mt19937_64 &rng, std::
     side.swap(best);
 }
 
-// multilevel recursive bisection: parts [p0, p0 + np) over the vertices `verts` of g
-void recursive_bisect(const Graph &g, const std::vector<int32_t> &verts, int p0, int np, double ub,
-                      std::mt19937_64 &rng, std::vector<int32_t> &l, std::vector<int32_t> &part, int *levels,
-                      int *coarse_n) {
+// multilevel recursive bisection: parts [p0, p0 + np) over the vertices `verts` of g.  Each sub-problem draws from
+// its own generator seeded by (seed, p0, np), so the two halves can run on two threads and the result does not
+// depend on scheduling; the first log2(8) levels fork (a k = 8 partition keeps up to 4 threads busy).
+struct RbStats {
+    std::mutex mu;
+    int levels = 0, coarse_n = 0;
+};
+void recursive_bisect(const Graph &g, const std::vector<int32_t> &verts, int p0, int np, double ub, uint64_t seed,
+                      std::vector<int32_t> &part, RbStats &st, int depth) {
     if (np == 1 || verts.size() <= 1) {
         for (int v : verts) part[v] = p0;
         return;
@@ -376,15 +393,29 @@ void recursive_bisect(const Graph &g, const std::vector<int32_t> &verts, int p0,
     const int nl = np / 2;
     std::vector<int8_t> side;
     {
+        std::mt19937_64 rng(seed ^ (0x9E3779B97F4A7C15ull * (uint64_t)(p0 + 1)) ^ ((uint64_t)np << 40));
+        std::vector<int32_t> l(g.n, -1);
         Graph s = induced(g, verts, l);
+        std::vector<int32_t>().swap(l);
         // the per-bisection slack compounds over log2(k) levels: split the 1.03 budget between them
         const double lvl_ub = std::pow(ub, 1.0 / std::max(1.0, std::ceil(std::log2((double)np))));
-        ml_bisect(s, (double)nl / np, lvl_ub, rng, side, levels, coarse_n);
+        int levels = 0, coarse_n = 0;
+        ml_bisect(s, (double)nl / np, lvl_ub, rng, side, &levels, &coarse_n);
+        std::lock_guard<std::mutex> lk(st.mu);
+        st.levels = std::max(st.levels, levels);
+        st.coarse_n = std::max(st.coarse_n, coarse_n);
     }
     std::vector<int32_t> L, R;
     for (size_t v = 0; v < verts.size(); v++) (side[v] == 0 ? L : R).push_back(verts[v]);
-    recursive_bisect(g, L, p0, nl, ub, rng, l, part, levels, coarse_n);
-    recursive_bisect(g, R, p0 + nl, np - nl, ub, rng, l, part, levels, coarse_n);
+    std::vector<int8_t>().swap(side);
+    if (depth < 3 && nl > 0 && np - nl > 1) {
+        std::thread t([&] { recursive_bisect(g, L, p0, nl, ub, seed, part, st, depth + 1); });
+        recursive_bisect(g, R, p0 + nl, np - nl, ub, seed, part, st, depth + 1);
+        t.join();
+    } else {
+        recursive_bisect(g, L, p0, nl, ub, seed, part, st, depth + 1);
+        recursive_bisect(g, R, p0 + nl, np - nl, ub, seed, part, st, depth + 1);
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -617,13 +648,23 @@ static int partition_one(const ShudMeshSoA *mesh, const double *cx, const double
         S.graph_cut = -1;                                       // reported for the multilevel graph only
     } else if (method == SHUD_PART_MULTILEVEL) {
         const double ub = 1.03;
-        std::mt19937_64 rng(seed);
+        const bool verbose = getenv("SHUD_PART_VERBOSE") != nullptr;
+        auto tk = std::chrono::steady_clock::now();
+        auto lap = [&](const char *what) {
+            const auto now = std::chrono::steady_clock::now();
+            if (verbose) fprintf(stderr, "[partition] %s %.2fs\n", what, std::chrono::duration<double>(now - tk).count());
+            tk = now;
+        };
         Graph g = dual_graph(mesh);
-        std::vector<int32_t> part(NE, 0), all(NE), l(NE, -1);
+        lap("dual graph");
+        std::vector<int32_t> part(NE, 0), all(NE);
         std::iota(all.begin(), all.end(), 0);
-        int levels = 0, coarse_n = 0;
-        recursive_bisect(g, all, 0, nparts, ub, rng, l, part, &levels, &coarse_n);
+        RbStats rb;
+        recursive_bisect(g, all, 0, nparts, ub, seed, part, rb, 0);
+        const int levels = rb.levels, coarse_n = rb.coarse_n;
+        lap("recursive bisection");
         kway_refine(g, nparts, ub, 8, part);                    // k-way polish of the assembled partition
+        lap("k-way refinement");
         S.levels = levels;
         S.coarse_vertices = coarse_n;
         S.graph_cut = graph_cut(g, part);
