@@ -359,11 +359,14 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         cls[i] = it->second;
     }
     const int ncls = (int)table.size();
-    // beyond what one workgroup's LDS copy holds, the class lookups become dependent L2 trips: measured on
-    // syn-10M with 13,200 classes, 1.47 ms per element kernel against 1.05 ms for the SoA kernel
-    // (bench.py many_class) -> SoA, unless SHUD_RHS_L2_CLASS=1 asks for the L2 table (A/B, bench)
+    // beyond what one workgroup's LDS copy holds (128 classes) the class lookups become dependent L2 trips.
+    // Measured on syn-10M (tools/class_sweep.py, profiles/r02/class_sweep.log): element kernel 0.65 ms with
+    // 33 classes in LDS; from L2 0.83 ms at 132 classes, 1.21 at 495, 1.49 at 1,980, 1.66 at 13,200; the SoA
+    // kernel 1.09 ms at any count -> the L2 table up to 256 classes, SoA above (SHUD_RHS_L2_CLASS=1 forces the
+    // L2 table, =0 forces SoA above 128: A/B and bench.py many_class)
     const char *l2 = getenv("SHUD_RHS_L2_CLASS");
-    if (ncls > kLdsClassMax && !(l2 && l2[0] == '1')) return 0;
+    const int l2_max = (l2 && l2[0] == '1') ? 32768 : (l2 && l2[0] == '0') ? kLdsClassMax : 256;
+    if (ncls > l2_max) return 0;
     std::vector<double> ctab((size_t)CF_STRIDE * ncls, 0.0);
     for (int c = 0; c < ncls; c++) {
         std::vector<double> &t = table[c];

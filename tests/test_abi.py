@@ -60,3 +60,29 @@ def test_struct_layouts_match_header():
                       ("ShudEtOut", abi.ShudEtOut), ("ShudOdeOptions", abi.ShudOdeOptions),
                       ("ShudOdeStats", abi.ShudOdeStats), ("ShudPrintSpec", abi.ShudPrintSpec)]:
         assert C.sizeof(cls) == _c_sizeof(name), name
+
+
+def test_host_library_exports_partition_symbols():
+    """libshud_host.so exports every function include/shud_partition.h and shud_host.h declare; the ctypes
+    mirrors of ShudPartStats / ShudPlanInfo match the C layout."""
+    from shud_rhs import partition
+    lib_path = os.path.join(ROOT, "shud-up_amd", "libshud_host.so")
+    if not os.path.exists(lib_path):
+        subprocess.check_call(["make", "-C", os.path.join(ROOT, "shud-up_amd"), "libshud_host.so"])
+    lib = C.CDLL(lib_path)
+    for h, prefix in (("shud_partition.h", r"shud_(?:partition|plan)_"), ("shud_host.h", r"shud_project_")):
+        txt = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", h)).read(), flags=re.S)
+        names = set(re.findall(r"\b(" + prefix + r"\w+)\s*\(", txt))
+        assert len(names) >= 5, h
+        for n in names:
+            assert hasattr(lib, n), n
+    partition._host()                     # binds every partitioner symbol with its signature
+    for name, cls in (("ShudPartStats", partition.ShudPartStats), ("ShudPlanInfo", partition.ShudPlanInfo)):
+        src = (f'#include "shud_partition.h"\n#include <stdio.h>\n'
+               f'int main(){{printf("%zu\\n", sizeof({name}));return 0;}}\n')
+        exe = f"/tmp/sz_{name}_{os.getpid()}"
+        subprocess.run(["gcc", "-x", "c", "-", "-I", os.path.join(ROOT, "include"), "-o", exe], input=src.encode(),
+                       check=True)
+        out = int(subprocess.check_output([exe]).decode().strip())
+        os.unlink(exe)
+        assert out == C.sizeof(cls), (name, out, C.sizeof(cls))
