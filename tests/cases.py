@@ -84,3 +84,49 @@ def states(m, y0=None, n_random=4, seed=100):
     for k in range(n_random):
         out.append(workload.random_state(m, seed=seed + k))
     return out
+
+
+def _subset(m, keep, close_boundary=None):
+    """elements `keep` of m (neighbours outside become boundary edges), no rivers"""
+    from shud_rhs import ShudModel
+    keep = np.asarray(keep)
+    NE = m.num_ele
+    g2l = np.full(NE, -1, dtype=np.int64)
+    g2l[keep] = np.arange(keep.size)
+    r = ShudModel(keep.size, 0, 0, m.close_boundary if close_boundary is None else close_boundary)
+    for k, v in m.ele.items():
+        r.ele[k] = v.reshape(3, -1)[:, keep].reshape(-1) if v.size == 3 * NE else v[keep]
+    nab = m.nabr.reshape(3, -1)[:, keep]
+    r.nabr = np.where(nab >= 0, g2l[np.where(nab >= 0, nab, 0)], -1).reshape(-1).astype(np.int32)
+    # an edge whose neighbour was dropped is a boundary edge: avgRough = the element's own Rough there
+    # (Element.cpp:249-265)
+    cut = (r.nabr.reshape(3, -1) < 0) & (nab >= 0)
+    ar = r.ele["avg_rough"].reshape(3, -1).copy()
+    ar[cut] = np.broadcast_to(r.ele["rough"], ar.shape)[cut]
+    r.ele["avg_rough"] = ar.reshape(-1)
+    r.ibc, r.iss = m.ibc[keep], m.iss[keep]
+    r.par = {k: v[keep] for k, v in m.par.items()}
+    r.step = {k: v[keep] for k, v in m.step.items()}
+    r.riv = {}
+    r.riv_down = np.zeros(0, np.int32)
+    r.riv_bc = np.zeros(0, np.int32)
+    r.seg_ele = np.zeros(0, np.int32)
+    r.seg_riv = np.zeros(0, np.int32)
+    r.seg_length = np.zeros(0)
+    r.seg_cwr = np.zeros(0)
+    return r.finalize()
+
+
+def riverless():
+    """ccw without its river network (NR = NS = 0): element fluxes only."""
+    m, y0 = ccw()
+    return _subset(m, np.arange(m.num_ele)), y0[:3 * m.num_ele].copy()
+
+
+def single_element(close_boundary=0):
+    """one triangle, every edge a domain boundary (the open-boundary outflow of MD_ElementFlux.cpp:81-93,
+    139-152 on all three edges when close_boundary = 0)."""
+    m, y0 = ccw()
+    r = _subset(m, np.array([5]), close_boundary)
+    y = np.array([0.03, 0.4 * r.par["aquifer_depth"][0], 0.6 * r.par["aquifer_depth"][0]])
+    return r, y

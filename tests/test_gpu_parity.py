@@ -238,3 +238,20 @@ def test_many_classes(oracle_mod, monkeypatch, l2):
     for mode in (abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP):
         _compare_sequence(m, [y] + cases.states(m, None, 1, seed=3), mode, oracle_mod, ncalls=2,
                           label=f"many-class l2={l2}", layout="packed" if l2 == "1" else "soa")
+
+
+@pytest.mark.parametrize("mode", [abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP])
+def test_edge_meshes(mode, oracle_mod, layout):
+    """Edge cases of the mesh: no rivers at all (NR = NS = 0, empty river launch), the smallest synthetic meshes
+    (8 and 48 elements, every element on or next to the boundary), and a single triangle whose three edges are
+    all open boundaries."""
+    from shud_rhs import synth
+    cases_ = [("riverless ccw",) + cases.riverless(), ("single open", *cases.single_element(0)),
+              ("single closed", *cases.single_element(1))]
+    for n in (2, 50):
+        m = synth.synth_model(n)
+        m.step = workload.random_step_inputs(m, seed=n)
+        cases_.append((f"synth {m.num_ele}", m, workload.random_state(m, seed=n)))
+    for label, m, y in cases_:
+        _compare_sequence(m, [y] + cases.states(m, None, 2, seed=31), mode, oracle_mod, ncalls=2, label=label,
+                          layout=layout)

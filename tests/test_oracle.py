@@ -23,7 +23,7 @@ def _bit_equal(a, b):
     return bool(np.all((a == b) | (np.isnan(a) & np.isnan(b))))
 
 
-@pytest.mark.parametrize("case", ["ccw", "heihe", "variant"])
+@pytest.mark.parametrize("case", ["ccw", "heihe", "variant", "riverless", "single_element"])
 @pytest.mark.parametrize("mode", [abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP])
 def test_two_restatements_bit_identical(case, mode):
     m, y = getattr(cases, case)()
