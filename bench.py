@@ -120,9 +120,10 @@ def main():
     for _ in range(args.warmup):
         h.eval_device(0.0, yp, dyp)
     torch.cuda.synchronize()
-    # HIP events around the kernels of every 5th timed eval (handle's stream = torch's current stream): an event
-    # between two kernels stops their tails overlapping, so only a sample of the K evals carries them
-    t_stride = 5 if args.steps >= 20 else 1
+    # HIP events around the kernels of every 2nd timed eval (handle's stream = torch's current stream): an event
+    # between two kernels stops their tails overlapping (~1 % of an eval), so only a sample of the K evals
+    # carries them
+    t_stride = 2 if args.steps >= 10 else 1
     h.timing(args.steps, t_stride)
     if world > 1:
         dist.barrier()
@@ -194,7 +195,7 @@ def main():
             "algorithmic_bytes_per_launch": ele_bytes,
             "kernel_ms": {k: v for k, v in per.items()},
             "kernel_ms_source": (f"HIP events around the kernels of {n_timed} of the {args.steps} timed evals "
-                                 f"(every {t_stride}th; handle stream)"),
+                                 f"(1 in {t_stride}; handle stream)"),
             "rhs_frac": (ele_bytes + riv_bytes) / (ms_eval * 1e-3) / HBM_PEAK,
             "riv_algorithmic_bytes_per_launch": riv_bytes,
             "riv_frac": riv_bytes / (ms_riv * 1e-3) / HBM_PEAK if ms_riv > 0 else None,
