@@ -63,7 +63,7 @@ def _run_ranks(m, y_list, locs, mode, ncalls=3):
                     hs[r].eval_compute(0.0, bufs[r][0], bufs[r][1])
                     got = hs[r].d2h(np.zeros(bufs[r][2]), bufs[r][1])
                     want = partition.local_state(ref, m, part)
-                    assert np.array_equal(got, want), f"rank {r} call {call}: {(got != want).sum()} differ"
+                    assert np.array_equal(got, want, equal_nan=True), f"rank {r} call {call}: {(got != want).sum()} differ"
     finally:
         for h, (a, b, _) in zip(hs, bufs):
             h.device_free(a)
@@ -93,6 +93,20 @@ def test_cpp_plans_bit_identical(nranks, method):
     locs = [partition.CppPlan(m, ep, nranks, r).local_model() for r in range(nranks)]
     for mode in (0, 1):
         _run_ranks(m, [y, workload.random_state(m, seed=5)], locs, mode, ncalls=2)
+
+
+@pytest.mark.parametrize("nranks", [3, 5])
+@pytest.mark.parametrize("seed", [2, 9])
+def test_ragged_random_partitions(nranks, seed):
+    """Random element-to-rank assignments (disconnected, ragged parts: every element can be a boundary element,
+    every reach split) through the C++ planner: still bit-identical (NaNs of negative outlet stages included)."""
+    m, y = cases.variant(6000, seed=seed)
+    rng = np.random.default_rng(seed)
+    ep = rng.integers(0, nranks, m.num_ele).astype(np.int32)
+    ep[:nranks] = np.arange(nranks)
+    locs = [partition.CppPlan(m, ep, nranks, r).local_model() for r in range(nranks)]
+    for mode in (0, 1):
+        _run_ranks(m, [y, workload.random_state(m, seed=seed + 1)], locs, mode, ncalls=2)
 
 
 @pytest.mark.parametrize("nranks", [2, 8])

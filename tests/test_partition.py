@@ -97,7 +97,7 @@ def test_k_rank_simulation_bit_identical(nranks, mode, planner):
                 dy_ext = from_o(o.eval(0.0, to_o(partition.extended_state(owned[r], gele, griv, part)))[0])
                 got = partition.owned_dy(dy_ext, lm, part)
                 want = partition.local_state(ref, m, part)
-                assert np.array_equal(got, want), f"rank {r} call {call}"
+                assert np.array_equal(got, want, equal_nan=True), f"rank {r} call {call}"
 
 
 @pytest.mark.parametrize("nranks", [2, 4, 8])
