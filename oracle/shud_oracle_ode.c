@@ -153,11 +153,12 @@ static void v_linear_sum(long n, double a, const double *x, double b, const doub
 
 /* Reduction order.  0: the serial N_Vector's (one left-to-right sum, nvector_serial.c) — CVODE's own order.
  * 1: the device integrator's fixed order (shud-up_amd/csrc/shud_ode_kernels.hip): a grid of
- * B = min(ceil(n/256), 2048) blocks x 256 threads; thread (b, t) sums entries b*256 + t + k*256*B in k order from
+ * B = min(ceil(n/256), ORACLE_RED_BLOCKS) blocks x 256 threads; thread (b, t) sums entries b*256 + t + k*256*B in k order from
  * 0.0; each 64-lane wave combines by an xor butterfly (offsets 32..1, own value first) and lane 0 keeps the
  * result; the block adds its 4 wave results in wave order; a one-block pass then does the same over the B
  * block partials.  With order 1 the restatement reproduces the device integrator bit for bit wherever the RHS
  * is IEEE-exact (tests/test_gpu_ode.py). */
+#define ORACLE_RED_BLOCKS 2048   /* shud_ode_dev.h kMaxBlocks (8192 measured: no faster reductions, finalize 6 -> 17 us) */
 static int g_red_order = 0;
 void oracle_ode_set_reduction_order(int order) { g_red_order = order; }
 
@@ -179,8 +180,9 @@ static double block_combine(double *lanes) {     /* lanes[256] -> 4 wave results
 static double device_order_sum(long n, const double *term) {
     long nb = (n + 255) / 256;
     if (nb < 1) nb = 1;
-    if (nb > 2048) nb = 2048;
-    double part[2048], lanes[256];
+    if (nb > ORACLE_RED_BLOCKS) nb = ORACLE_RED_BLOCKS;
+    static double part[ORACLE_RED_BLOCKS];
+    double lanes[256];
     for (long b = 0; b < nb; ++b) {
         for (int t = 0; t < 256; ++t) {
             double acc = 0.0;

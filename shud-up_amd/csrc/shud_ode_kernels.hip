@@ -1,13 +1,16 @@
 // shud_ode_kernels.hip — device vector kernels of the integrator (see shud_ode_dev.h).
 //
-// Streaming passes over fp64 vectors of NY entries (grid-stride, 256-thread blocks, grid fixed per NY so every
-// reduction is deterministic).  Per element each kernel applies exactly the serial N_Vector operations CVODE
+// Streaming passes over fp64 vectors of NY entries (256-thread blocks).  Reductions run on a grid fixed per NY
+// (grid_blocks) with a grid-stride loop, so every reduction is deterministic (stream<U> can issue the loads of
+// U consecutive iterations before consuming the first, at the same accumulation order).  Element-wise passes
+// run one entry per thread on a full grid.  Per element each kernel applies exactly the serial N_Vector operations CVODE
 // issues (nvector_serial.c: N_VLinearSum special cases, N_VScale, N_VProd/N_VDiv, N_VLinearCombination,
 // N_VScaleAddMulti) in the same order; the host controller (shud_ode.cpp) cites the CVODE routine each call
 // replaces.  The bound is HBM bandwidth: bytes per entry are listed at each kernel.
 #include "shud_ode_dev.h"
 
 #include <cmath>
+#include <cstdlib>
 
 namespace shud {
 namespace ode {
@@ -18,7 +21,54 @@ int grid_blocks(int64_t n) {
     return (int)(b < kMaxBlocks ? b : kMaxBlocks);
 }
 
-#define GRID_LOOP(i, n) for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < (n); i += (int64_t)gridDim.x * kThreads)
+// reduction kernels: loads issued per thread before the first is consumed.  SHUD_ODE_UNROLL=4 measured slower
+// than 1 at syn-10M (mgs 149 -> 177 us, ewt 105 -> 147 us), so 1 is the default.
+static int unroll() {
+    static const int u = [] {
+        const char *e = getenv("SHUD_ODE_UNROLL");
+        return e && atoi(e) == 4 ? 4 : 1;
+    }();
+    return u;
+}
+// element-wise grid: one entry per thread (full occupancy; measured 15-20% faster than the 2048-block
+// grid-stride loop at syn-10M: dq_work 214 -> 179 us, pascal<3> 395 -> 323 us)
+static int ew_blocks(int64_t n) {
+    const int64_t b = (n + kThreads - 1) / kThreads;
+    return (int)(b < 1 ? 1 : b);
+}
+
+// Grid-stride loop over [0, n): use(i, load(i)) for the thread's indices in increasing order, the loads of U
+// consecutive iterations issued before any of them is used.  T is the per-index operand bundle.
+template <int U, class T, class Load, class Use>
+__device__ __forceinline__ void stream(int64_t n, Load load, Use use) {
+    const int64_t st = (int64_t)gridDim.x * kThreads;
+    int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if constexpr (U > 1) {
+        for (; i + (U - 1) * st < n; i += U * st) {
+            T a[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) a[u] = load(i + u * st);
+#pragma unroll
+            for (int u = 0; u < U; ++u) use(i + u * st, a[u]);
+        }
+    }
+    for (; i < n; i += st) use(i, load(i));
+}
+struct D1 { double a; };
+struct D2 { double a, b; };
+struct D3 { double a, b, c; };
+struct D4 { double a, b, c, d; };
+template <int N>
+struct DN { double v[N]; };
+
+// reduction kernel template K<U> on the fixed reduction grid, U = unroll()
+#define LAUNCH_RED(K, r, s, ...)                                                    \
+    do {                                                                            \
+        if (unroll() == 1) K<1><<<(r).nblk, kThreads, 0, (s)>>>(__VA_ARGS__, (r));  \
+        else K<4><<<(r).nblk, kThreads, 0, (s)>>>(__VA_ARGS__, (r));                \
+    } while (0)
+// element-wise kernel: one load batch per iteration on the ew_blocks grid
+#define LAUNCH_EW(K, n, s, ...) K<1><<<ew_blocks(n), kThreads, 0, (s)>>>(n, __VA_ARGS__)
 
 __device__ inline double comb(double a, double b, bool mn) { return mn ? fmin(a, b) : a + b; }
 
@@ -82,90 +132,111 @@ void finalize(const Red &r, int nacc, unsigned minmask, hipStream_t s) {
 }
 
 // cvEwtSetSS + the N_VWrmsNorm(zn[0], ewt) of CVode's "too much accuracy" check.  24 B/entry.
+template <int U>
 __global__ void __launch_bounds__(kThreads) k_ewt(int64_t n, const double *__restrict__ zn0, double *__restrict__ ewt,
                                                   double rtol, double atol, Red r) {
     double v[2] = {INFINITY, 0.0};
-    GRID_LOOP(i, n) {
-        const double y = zn0[i];
+    stream<U, D1>(n, [&](int64_t i) { return D1{zn0[i]}; }, [&](int64_t i, const D1 &o) {
+        const double y = o.a;
         const double t = rtol * fabs(y) + atol;
         const double w = 1.0 / t;
         ewt[i] = w;
         v[0] = fmin(v[0], t);
         const double p = y * w;
         v[1] += p * p;
-    }
+    });
     block_partial<2>(v, 1u, r);
 }
 void ewt_set(int64_t n, const double *zn0, double *ewt, double rtol, double atol, const Red &r, hipStream_t s) {
-    k_ewt<<<r.nblk, kThreads, 0, s>>>(n, zn0, ewt, rtol, atol, r);
+    LAUNCH_RED(k_ewt, r, s, n, zn0, ewt, rtol, atol);
 }
 
 // cvPredict / cvRestore: Pascal-triangle update of the Nordsieck array in registers.  2*8*(q+1) B/entry.
-template <int Q, bool FWD>
+template <int Q, bool FWD, int U>
 __global__ void __launch_bounds__(kThreads) k_pascal(int64_t n, double *__restrict__ zn) {
-    GRID_LOOP(i, n) {
-        double a[Q + 1];
+    using T = DN<Q + 1>;
+    stream<U, T>(n, [&](int64_t i) {
+        T a;
 #pragma unroll
-        for (int j = 0; j <= Q; ++j) a[j] = zn[(int64_t)j * n + i];
+        for (int j = 0; j <= Q; ++j) a.v[j] = zn[(int64_t)j * n + i];
+        return a;
+    }, [&](int64_t i, T a) {
 #pragma unroll
         for (int k = 1; k <= Q; ++k)
 #pragma unroll
-            for (int j = Q; j >= k; --j) a[j - 1] = FWD ? a[j - 1] + a[j] : a[j - 1] - a[j];
+            for (int j = Q; j >= k; --j) a.v[j - 1] = FWD ? a.v[j - 1] + a.v[j] : a.v[j - 1] - a.v[j];
 #pragma unroll
-        for (int j = 0; j < Q; ++j) zn[(int64_t)j * n + i] = a[j];
-    }
+        for (int j = 0; j < Q; ++j) zn[(int64_t)j * n + i] = a.v[j];
+    });
+}
+template <int Q, bool FWD>
+static void pascal_q(int64_t n, double *zn, hipStream_t s) {
+    k_pascal<Q, FWD, 1><<<ew_blocks(n), kThreads, 0, s>>>(n, zn);
 }
 template <bool FWD>
 static void pascal(int64_t n, double *zn, int q, hipStream_t s) {
-    const int g = grid_blocks(n);
     switch (q) {
-    case 1: k_pascal<1, FWD><<<g, kThreads, 0, s>>>(n, zn); break;
-    case 2: k_pascal<2, FWD><<<g, kThreads, 0, s>>>(n, zn); break;
-    case 3: k_pascal<3, FWD><<<g, kThreads, 0, s>>>(n, zn); break;
-    case 4: k_pascal<4, FWD><<<g, kThreads, 0, s>>>(n, zn); break;
-    default: k_pascal<5, FWD><<<g, kThreads, 0, s>>>(n, zn); break;
+    case 1: pascal_q<1, FWD>(n, zn, s); break;
+    case 2: pascal_q<2, FWD>(n, zn, s); break;
+    case 3: pascal_q<3, FWD>(n, zn, s); break;
+    case 4: pascal_q<4, FWD>(n, zn, s); break;
+    default: pascal_q<5, FWD>(n, zn, s); break;
     }
 }
 void predict(int64_t n, double *zn, int q, hipStream_t s) { pascal<true>(n, zn, q, s); }
 void restore(int64_t n, double *zn, int q, hipStream_t s) { pascal<false>(n, zn, q, s); }
 
 // cvRescale: zn[j] *= eta^j (N_VScaleVectorArray).  16*q B/entry.
+template <int U>
 __global__ void __launch_bounds__(kThreads) k_rescale(int64_t n, double *__restrict__ zn, int q, Coefs c) {
-    GRID_LOOP(i, n) {
-        for (int j = 1; j <= q; ++j) zn[(int64_t)j * n + i] *= c.c[j];
-    }
+    using T = DN<kQMax>;
+    stream<U, T>(n, [&](int64_t i) {
+        T a;
+#pragma unroll
+        for (int j = 1; j <= kQMax; ++j)
+            if (j <= q) a.v[j - 1] = zn[(int64_t)j * n + i];
+        return a;
+    }, [&](int64_t i, const T &a) {
+#pragma unroll
+        for (int j = 1; j <= kQMax; ++j)
+            if (j <= q) zn[(int64_t)j * n + i] = a.v[j - 1] * c.c[j];
+    });
 }
 void rescale(int64_t n, double *zn, int q, const Coefs &c, hipStream_t s) {
-    k_rescale<<<grid_blocks(n), kThreads, 0, s>>>(n, zn, q, c);
+    LAUNCH_EW(k_rescale, n, s, zn, q, c);
 }
 
+template <int U>
 __global__ void __launch_bounds__(kThreads) k_vsum(int64_t n, const double *__restrict__ x, const double *__restrict__ y,
                                                    double *__restrict__ z) {
-    GRID_LOOP(i, n) z[i] = x[i] + y[i];
+    stream<U, D2>(n, [&](int64_t i) { return D2{x[i], y[i]}; }, [&](int64_t i, const D2 &o) { z[i] = o.a + o.b; });
 }
 void vsum(int64_t n, const double *x, const double *y, double *z, hipStream_t s) {
-    k_vsum<<<grid_blocks(n), kThreads, 0, s>>>(n, x, y, z);
+    LAUNCH_EW(k_vsum, n, s, x, y, z);
 }
 // cvNls's N_VConst(0, ycor) fused into cvNlsResidual's N_VLinearSum(1, zn[0], 1, ycor, y): ycor = 0 and
 // z = x + 0.0 (the same add as k_vsum with a zero operand, so -0.0 becomes +0.0 exactly as there).  24 B/entry
 // instead of a 8 B/entry fill plus 24 B/entry.
+template <int U>
 __global__ void __launch_bounds__(kThreads) k_vsum_zero(int64_t n, const double *__restrict__ x,
                                                         double *__restrict__ ycor, double *__restrict__ z) {
-    GRID_LOOP(i, n) {
+    stream<U, D1>(n, [&](int64_t i) { return D1{x[i]}; }, [&](int64_t i, const D1 &o) {
         const double zero = 0.0;
         ycor[i] = zero;
-        z[i] = x[i] + zero;
-    }
+        z[i] = o.a + zero;
+    });
 }
 void vsum_zero(int64_t n, const double *x, double *ycor, double *z, hipStream_t s) {
-    k_vsum_zero<<<grid_blocks(n), kThreads, 0, s>>>(n, x, ycor, z);
+    LAUNCH_EW(k_vsum_zero, n, s, x, ycor, z);
 }
 
+template <int U>
 __global__ void __launch_bounds__(kThreads) k_scale_to(int64_t n, double c, const double *x, double *z) {
-    GRID_LOOP(i, n) z[i] = c * x[i];
+    // x may alias z (N_VScale in place): each index is loaded before it is stored
+    stream<U, D1>(n, [&](int64_t i) { return D1{x[i]}; }, [&](int64_t i, const D1 &o) { z[i] = c * o.a; });
 }
 void scale_to(int64_t n, double c, const double *x, double *z, hipStream_t s) {
-    k_scale_to<<<grid_blocks(n), kThreads, 0, s>>>(n, c, x, z);
+    LAUNCH_EW(k_scale_to, n, s, c, x, z);
 }
 void copy(int64_t n, const double *x, double *z, hipStream_t s) {
     (void)hipMemcpyAsync(z, x, n * sizeof(double), hipMemcpyDeviceToDevice, s);
@@ -173,74 +244,91 @@ void copy(int64_t n, const double *x, double *z, hipStream_t s) {
 void zero(int64_t n, double *z, hipStream_t s) { (void)hipMemsetAsync(z, 0, n * sizeof(double), s); }
 
 // cvIncreaseBDF / cvDecreaseBDF: zn[j] = coef[j]*zn[src] + zn[j] (N_VScaleAddMulti / Vaxpy)
+template <int U>
 __global__ void __launch_bounds__(kThreads) k_axpy_multi(int64_t n, double *__restrict__ zn, int src, Coefs c, int jlo,
                                                          int jhi) {
-    GRID_LOOP(i, n) {
-        const double x = zn[(int64_t)src * n + i];
-        for (int j = jlo; j <= jhi; ++j) zn[(int64_t)j * n + i] = c.c[j] * x + zn[(int64_t)j * n + i];
-    }
+    using T = DN<kQMax + 2>;              // [0]: zn[src]; [j]: zn[j], j in [jlo, jhi] (1 <= jlo)
+    stream<U, T>(n, [&](int64_t i) {
+        T a;
+        a.v[0] = zn[(int64_t)src * n + i];
+#pragma unroll
+        for (int j = 1; j <= kQMax + 1; ++j)
+            if (j >= jlo && j <= jhi) a.v[j] = zn[(int64_t)j * n + i];
+        return a;
+    }, [&](int64_t i, const T &a) {
+#pragma unroll
+        for (int j = 1; j <= kQMax + 1; ++j)
+            if (j >= jlo && j <= jhi) zn[(int64_t)j * n + i] = c.c[j] * a.v[0] + a.v[j];
+    });
 }
 void axpy_multi(int64_t n, double *zn, int src, const Coefs &coef, int jlo, int jhi, hipStream_t s) {
     if (jhi < jlo) return;
-    k_axpy_multi<<<grid_blocks(n), kThreads, 0, s>>>(n, zn, src, coef, jlo, jhi);
+    LAUNCH_EW(k_axpy_multi, n, s, zn, src, coef, jlo, jhi);
 }
 
 // cvNlsResidual (res = rl1*zn[1] + ycor; res += (-gamma)*ftemp) + Newton's N_VScale(-1, delta, delta)
 // + cvLsSolve's N_VWrmsNorm(b, ewt) (= SPGMR's ||s1*b||_2 / sqrt(N)).  40 B/entry.
+template <int U>
 __global__ void __launch_bounds__(kThreads) k_residual(int64_t n, const double *__restrict__ zn1,
                                                        const double *__restrict__ ycor, const double *__restrict__ ftemp,
                                                        double rl1, double ngamma, const double *__restrict__ ewt,
                                                        double *__restrict__ delta, Red r) {
     double v[1] = {0.0};
-    GRID_LOOP(i, n) {
-        const double r1 = rl1 * zn1[i] + (ycor ? ycor[i] : 0.0);     // ycor == nullptr: ycor is all +0.0
-        const double r2 = r1 + ngamma * ftemp[i];
+    stream<U, D4>(n, [&](int64_t i) {
+        return D4{zn1[i], ycor ? ycor[i] : 0.0, ftemp[i], ewt[i]};      // ycor == nullptr: ycor is all +0.0
+    }, [&](int64_t i, const D4 &o) {
+        const double r1 = rl1 * o.a + o.b;
+        const double r2 = r1 + ngamma * o.c;
         const double d = -r2;
         delta[i] = d;
-        const double p = d * ewt[i];
+        const double p = d * o.d;
         v[0] += p * p;
-    }
+    });
     block_partial<1>(v, 0u, r);
 }
 void residual(int64_t n, const double *zn1, const double *ycor, const double *ftemp, double rl1, double ngamma,
               const double *ewt, double *delta, const Red &r, hipStream_t s) {
-    k_residual<<<r.nblk, kThreads, 0, s>>>(n, zn1, ycor, ftemp, rl1, ngamma, ewt, delta, r);
+    LAUNCH_RED(k_residual, r, s, n, zn1, ycor, ftemp, rl1, ngamma, ewt, delta);
 }
 
 // SPGMR: vtemp = s1*r0; V[0] = (1/r_norm)*vtemp; and the WRMS norm of V[0]/s2 for the first DQ perturbation.
+template <int U>
 __global__ void __launch_bounds__(kThreads) k_krylov_v0(int64_t n, const double *__restrict__ delta,
                                                         const double *__restrict__ ewt, double c,
                                                         double *__restrict__ V0, Red r) {
     double v[1] = {0.0};
-    GRID_LOOP(i, n) {
-        const double w = ewt[i];
-        const double x = c * (w * delta[i]);
+    stream<U, D2>(n, [&](int64_t i) { return D2{ewt[i], delta[i]}; }, [&](int64_t i, const D2 &o) {
+        const double w = o.a;
+        const double x = c * (w * o.b);
         V0[i] = x;
         const double p = (x / w) * w;
         v[0] += p * p;
-    }
+    });
     block_partial<1>(v, 0u, r);
 }
 void krylov_v0(int64_t n, const double *delta, const double *ewt, double c, double *V0, const Red &r, hipStream_t s) {
-    k_krylov_v0<<<r.nblk, kThreads, 0, s>>>(n, delta, ewt, c, V0, r);
+    LAUNCH_RED(k_krylov_v0, r, s, n, delta, ewt, c, V0);
 }
 
 __device__ inline double dq_sig(const double *ds, int64_t n) { return 1.0 / sqrt(ds[S_SIG] / (double)n); }
 
 // cvLsDQJtimes: work = sig*v + y with v = V[l]/s2 (N_VDiv) and sig = 1/||v||_wrms.  32 B/entry.
+template <int U>
 __global__ void __launch_bounds__(kThreads) k_dq_work(int64_t n, const double *__restrict__ V,
                                                       const double *__restrict__ ewt, const double *__restrict__ y,
                                                       double *__restrict__ work, const double *__restrict__ ds) {
     const double sig = dq_sig(ds, n);
-    GRID_LOOP(i, n) work[i] = sig * (V[i] / ewt[i]) + y[i];
+    stream<U, D3>(n, [&](int64_t i) { return D3{V[i], ewt[i], y[i]}; },
+                  [&](int64_t i, const D3 &o) { work[i] = sig * (o.a / o.b) + o.c; });
 }
 void dq_work(int64_t n, const double *V, const double *ewt, const double *y, double *work, const double *ds,
              hipStream_t s) {
-    k_dq_work<<<grid_blocks(n), kThreads, 0, s>>>(n, V, ewt, y, work, ds);
+    LAUNCH_EW(k_dq_work, n, s, V, ewt, y, work, ds);
 }
 
 // cvLsDQJtimes tail (Jv = siginv*(f(work) - fy)), cvLsATimes (z = v - gamma*Jv), SPGMR left scaling
 // (V[l+1] = s1*z), and the first two Gram-Schmidt reductions (||V[l+1]||^2, V[0].V[l+1]).  48 B/entry.
+template <int U>
 __global__ void __launch_bounds__(kThreads) k_atimes(int64_t n, double *__restrict__ w, const double *__restrict__ fy,
                                                      const double *__restrict__ V, const double *__restrict__ ewt,
                                                      const double *__restrict__ V0, double ngamma,
@@ -248,126 +336,167 @@ __global__ void __launch_bounds__(kThreads) k_atimes(int64_t n, double *__restri
     const double sig = dq_sig(ds, n);
     const double siginv = 1.0 / sig;
     double v[2] = {0.0, 0.0};
-    GRID_LOOP(i, n) {
-        const double e = ewt[i];
-        const double jv = siginv * (w[i] - fy[i]);
-        const double z = ngamma * jv + V[i] / e;
+    using T = DN<5>;
+    stream<U, T>(n, [&](int64_t i) { return T{{ewt[i], w[i], fy[i], V[i], V0[i]}}; }, [&](int64_t i, const T &o) {
+        const double e = o.v[0];
+        const double jv = siginv * (o.v[1] - o.v[2]);
+        const double z = ngamma * jv + o.v[3] / e;
         const double x = e * z;
         w[i] = x;
         v[0] += x * x;
-        v[1] += V0[i] * x;
-    }
+        v[1] += o.v[4] * x;
+    });
     block_partial<2>(v, 0u, r);
 }
 void atimes(int64_t n, double *w, const double *fy, const double *V, const double *ewt, const double *V0,
             double ngamma, const double *ds, const Red &r, hipStream_t s) {
-    k_atimes<<<r.nblk, kThreads, 0, s>>>(n, w, fy, V, ewt, V0, ngamma, ds, r);
+    LAUNCH_RED(k_atimes, r, s, n, w, fy, V, ewt, V0, ngamma, ds);
 }
 
 // SUNModifiedGS step: v[k] -= h[i-1] v[i-1] (N_VLinearSum -> Vaxpy), then h[i] = v[i].v[k] (or ||v[k]||^2).
+template <int U>
 __global__ void __launch_bounds__(kThreads) k_mgs(int64_t n, double *__restrict__ w, const double *__restrict__ Vprev,
                                                   const double *__restrict__ ds, int hslot,
                                                   const double *__restrict__ Vnext, Red r) {
     const double nh = Vprev ? -ds[hslot] : 0.0;
     double v[1] = {0.0};
-    GRID_LOOP(i, n) {
-        double x = w[i];
+    stream<U, D3>(n, [&](int64_t i) {
+        return D3{w[i], Vprev ? Vprev[i] : 0.0, Vnext ? Vnext[i] : 0.0};
+    }, [&](int64_t i, const D3 &o) {
+        double x = o.a;
         if (Vprev) {
-            x = x + nh * Vprev[i];
+            x = x + nh * o.b;
             w[i] = x;
         }
-        v[0] += Vnext ? Vnext[i] * x : x * x;
-    }
+        v[0] += Vnext ? o.c * x : x * x;
+    });
     block_partial<1>(v, 0u, r);
 }
 void mgs(int64_t n, double *w, const double *Vprev, const double *ds, int hslot, const double *Vnext, const Red &r,
          hipStream_t s) {
-    k_mgs<<<r.nblk, kThreads, 0, s>>>(n, w, Vprev, ds, hslot, Vnext, r);
+    LAUNCH_RED(k_mgs, r, s, n, w, Vprev, ds, hslot, Vnext);
 }
 
 // SPGMR: V[l+1] *= 1/h[l+1][l]; and the WRMS norm of V[l+1]/s2 for the next DQ perturbation.  24 B/entry.
+template <int U>
 __global__ void __launch_bounds__(kThreads) k_normalize(int64_t n, double *__restrict__ w, double c,
                                                         const double *__restrict__ ewt, Red r) {
     double v[1] = {0.0};
-    GRID_LOOP(i, n) {
-        const double x = w[i] * c;
+    stream<U, D2>(n, [&](int64_t i) { return D2{w[i], ewt[i]}; }, [&](int64_t i, const D2 &o) {
+        const double x = o.a * c;
         w[i] = x;
-        const double e = ewt[i];
+        const double e = o.b;
         const double p = (x / e) * e;
         v[0] += p * p;
-    }
+    });
     block_partial<1>(v, 0u, r);
 }
 void normalize(int64_t n, double *w, double c, const double *ewt, const Red &r, hipStream_t s) {
-    k_normalize<<<r.nblk, kThreads, 0, s>>>(n, w, c, ewt, r);
+    LAUNCH_RED(k_normalize, r, s, n, w, c, ewt);
 }
 
 // SPGMR solution xcor = sum_k yg[k] V[k] (N_VLinearCombination into xcor = 0), x = xcor/s2 (N_VDiv),
 // cvLsSolve's b = x, Newton's ycor += delta, and the convergence test's two WRMS norms.
+// (krydim <= kNuK here: SPGMR's maxl is 5; larger Krylov dimensions take the generic one-load-batch loop)
+constexpr int kNuK = 8;
+template <int U>
 __global__ void __launch_bounds__(kThreads) k_newton_update(int64_t n, const double *__restrict__ V, int64_t vstride,
                                                             int krydim, Coefs yg, const double *__restrict__ dsrc,
                                                             const double *__restrict__ ewt,
                                                             double *__restrict__ ycor, Red r) {
     double v[2] = {0.0, 0.0};
-    GRID_LOOP(i, n) {
-        const double e = ewt[i];
+    using T = DN<kNuK + 2>;               // [0] ewt, [1] ycor, [2] dsrc (krydim 0) or [2 + k] V[k]
+    const bool small = krydim <= kNuK;
+    stream<U, T>(n, [&](int64_t i) {
+        T a;
+        a.v[0] = ewt[i];
+        a.v[1] = ycor[i];
+        if (krydim == 0) {
+            a.v[2] = dsrc ? dsrc[i] : 0.0;
+        } else if (small) {
+#pragma unroll
+            for (int k = 0; k < kNuK; ++k)
+                if (k < krydim) a.v[2 + k] = V[k * vstride + i];
+        }
+        return a;
+    }, [&](int64_t i, const T &a) {
+        const double e = a.v[0];
         double d;
         if (krydim > 0) {
             double xc = 0.0;
-            for (int k = 0; k < krydim; ++k) xc = xc + yg.c[k] * V[k * vstride + i];
+            if (small) {
+#pragma unroll
+                for (int k = 0; k < kNuK; ++k)
+                    if (k < krydim) xc = xc + yg.c[k] * a.v[2 + k];
+            } else {
+                for (int k = 0; k < krydim; ++k) xc = xc + yg.c[k] * V[k * vstride + i];
+            }
             d = xc / e;
         } else {
-            d = dsrc ? dsrc[i] : 0.0;
+            d = a.v[2];
         }
-        const double yc = ycor[i] + d;
+        const double yc = a.v[1] + d;
         ycor[i] = yc;
         const double p = d * e, q = yc * e;
         v[0] += p * p;
         v[1] += q * q;
-    }
+    });
     block_partial<2>(v, 0u, r);
 }
 void newton_update(int64_t n, const double *V, int64_t vstride, int krydim, const Coefs &yg, const double *dsrc,
                    const double *ewt, double *ycor, const Red &r, hipStream_t s) {
-    k_newton_update<<<r.nblk, kThreads, 0, s>>>(n, V, vstride, krydim, yg, dsrc, ewt, ycor, r);
+    LAUNCH_RED(k_newton_update, r, s, n, V, vstride, krydim, yg, dsrc, ewt, ycor);
 }
 
 // cvCompleteStep: zn[j] = l[j]*acor + zn[j] (N_VScaleAddMulti), optional zn[qmax] = acor.
+template <int U>
 __global__ void __launch_bounds__(kThreads) k_complete(int64_t n, double *__restrict__ zn,
                                                        const double *__restrict__ acor, Coefs l, int q, int copy_to) {
-    GRID_LOOP(i, n) {
-        const double a = acor[i];
-        for (int j = 0; j <= q; ++j) zn[(int64_t)j * n + i] = l.c[j] * a + zn[(int64_t)j * n + i];
-        if (copy_to >= 0) zn[(int64_t)copy_to * n + i] = a;
-    }
+    using T = DN<kQMax + 2>;              // [0] acor, [1 + j] zn[j], j <= q
+    stream<U, T>(n, [&](int64_t i) {
+        T a;
+        a.v[0] = acor[i];
+#pragma unroll
+        for (int j = 0; j <= kQMax; ++j)
+            if (j <= q) a.v[1 + j] = zn[(int64_t)j * n + i];
+        return a;
+    }, [&](int64_t i, const T &a) {
+#pragma unroll
+        for (int j = 0; j <= kQMax; ++j)
+            if (j <= q) zn[(int64_t)j * n + i] = l.c[j] * a.v[0] + a.v[1 + j];
+        if (copy_to >= 0) zn[(int64_t)copy_to * n + i] = a.v[0];
+    });
 }
 void complete_step(int64_t n, double *zn, const double *acor, const Coefs &l, int q, int copy_to, hipStream_t s) {
-    k_complete<<<grid_blocks(n), kThreads, 0, s>>>(n, zn, acor, l, q, copy_to);
+    LAUNCH_EW(k_complete, n, s, zn, acor, l, q, copy_to);
 }
 
 // cvComputeEtaqm1 / cvComputeEtaqp1 norms in one pass
+template <int U>
 __global__ void __launch_bounds__(kThreads) k_eta_norms(int64_t n, const double *__restrict__ znq,
                                                         const double *__restrict__ znqmax,
                                                         const double *__restrict__ acor, double ncquot,
                                                         const double *__restrict__ ewt, Red r) {
     double v[2] = {0.0, 0.0};
-    GRID_LOOP(i, n) {
-        const double e = ewt[i];
+    stream<U, D4>(n, [&](int64_t i) {
+        return D4{ewt[i], znq ? znq[i] : 0.0, znqmax ? znqmax[i] : 0.0, znqmax ? acor[i] : 0.0};
+    }, [&](int64_t, const D4 &o) {
+        const double e = o.a;
         if (znq) {
-            const double p = znq[i] * e;
+            const double p = o.b * e;
             v[0] += p * p;
         }
         if (znqmax) {
-            const double t = ncquot * znqmax[i] + acor[i];
+            const double t = ncquot * o.c + o.d;
             const double p = t * e;
             v[1] += p * p;
         }
-    }
+    });
     block_partial<2>(v, 0u, r);
 }
 void eta_norms(int64_t n, const double *zn_q, const double *zn_qmax, const double *acor, double ncquot,
                const double *ewt, const Red &r, hipStream_t s) {
-    k_eta_norms<<<r.nblk, kThreads, 0, s>>>(n, zn_q, zn_qmax, acor, ncquot, ewt, r);
+    LAUNCH_RED(k_eta_norms, r, s, n, zn_q, zn_qmax, acor, ncquot, ewt);
 }
 
 // N_VLinearSum_Serial's case analysis for z distinct from x and y
@@ -391,7 +520,7 @@ struct Js {
 // CVodeGetDky: N_VLinearCombination(nvec, c, zn[js], dky), then N_VScale(h^-k, dky, dky) for k > 0
 __global__ void __launch_bounds__(kThreads) k_dky(int64_t n, const double *__restrict__ zn, int64_t stride, Js js,
                                                   Coefs c, int nvec, double rscale, double *__restrict__ out) {
-    GRID_LOOP(i, n) {
+    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
         double z;
         if (nvec == 1) {
             z = c.c[0] * zn[js.j[0] * stride + i];
