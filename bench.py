@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--settle", type=int, default=200,
+                    help="untimed RHS evals before the warm-up: a cold GPU's clocks wander for ~20 ms of load "
+                         "(element kernel 0.60 -> 0.65 -> 0.60 ms, profiles/r02/kt); same count on every rank")
     ap.add_argument("--n-ele", type=int, default=10_000_000)
     ap.add_argument("--mode", choices=["serial", "omp"], default="serial")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
@@ -117,6 +120,11 @@ def main():
     # GPU goes through in its first ~20 ms of load (element kernel 0.62 -> 0.74 -> 0.62 ms, profiles/r02/kt) then
     # falls outside the K timed evals instead of inside a short K = 20 window
     sp = stream_probe(local) if world == 1 else {}
+    ts = time.perf_counter()
+    for _ in range(args.settle):
+        h.eval_device(0.0, yp, dyp)
+    torch.cuda.synchronize()
+    settle_s = time.perf_counter() - ts
     for _ in range(args.warmup):
         h.eval_device(0.0, yp, dyp)
     torch.cuda.synchronize()
@@ -171,6 +179,8 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "settle": {"evals": args.settle, "seconds": round(settle_s, 3),
+                   "note": "untimed evals before the warm-up (clock settle), outside the timed region"},
         "ms_per_step": ms_step,
         "higher_is_better": True,
         "scaling": "strong",
