@@ -193,7 +193,7 @@ def main():
                                    f" partition, RCCL halo)") if world > 1 else "single GPU",
                    **({"edge_cut": cut_e, "segment_cut": cut_s, "max_halo_entities": pst["max_halo"],
                        "imbalance": pst["imbalance"]} if world > 1 else {}),
-                   "y_ydot": "device-resident"},
+                   "y_ydot": "device-resident", "kernel_layout": h.layout()},
         "roofline": {
             "bound": "hbm",
             "kernel": "shud_ele_kernel",

@@ -94,7 +94,8 @@ typedef struct ShudMeshSoA {
     /* lakes (MD_Lake.cpp, Lake.hpp/.cpp).  Lakes are on when any ilake > 0 (MD_readin.cpp:
      * 262-263); lake ids are 1..num_lake; a reach with riv_down <= -4 then flows into lake (-3 - down)
      * (MD_Lake.cpp:46-50) instead of the critical-depth outlet.  The y/ydot vectors gain num_lake stages
-     * after the reaches ([sf|us|gw|riv|lake], Macros.hpp:21-25).  Serial semantics, unpartitioned only. */
+     * after the reaches ([sf|us|gw|riv|lake], Macros.hpp:21-25).  Serial semantics; partitioned handles take
+     * the local mesh of shud_plan_local_mesh (owned lakes only, include/shud_partition.h). */
     int32_t num_lake;
     const int32_t *lake_bathy_off; /* [num_lake+1] row offsets of each lake's bathymetry table       */
     const double  *lake_bathy_y;   /* LakeBathymetry::yi (stage datum; zmin = yi[0]), lake_readBathy */

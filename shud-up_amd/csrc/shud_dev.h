@@ -113,7 +113,7 @@ struct DevDiag {                     // optional diagnostic outputs (ShudFluxOut
     double *q_lake_surf, *q_lake_sub, *q_lake_rivin, *q_lake_evap, *q_lake_prcp, *lake_toparea;
 };
 
-// ---- lakes (serial semantics, unpartitioned, packed layout) ----------------------------
+// ---- lakes (serial semantics, packed layout; partitioned: owned lakes) -------------------
 // Lake elements carry bit 31 of DevPacked::meta.w; a non-lake element's edge whose neighbour has it is a
 // bank edge (lakenabr, MD_Lake.cpp:131-143).  The element kernel writes each bank edge's fluxes; the lake
 // kernel reduces them, the lake elements' PET/precipitation and the inflowing reaches in reference order.

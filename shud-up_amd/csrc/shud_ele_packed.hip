@@ -616,10 +616,13 @@ void launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YV
     if (i1 <= i0) return;
     DevLake lk{};
     if (lake) lk = *lake;
-    // lakes: serial semantics only (the handle rejects OMP + lakes), class table in LDS
+    // lakes: serial semantics only (the handle rejects OMP + lakes), class table in LDS, with or without ghosts
     const bool gh = Y.gele != nullptr || Y.griv != nullptr;      // partitioned handle: ghost entities
 #define LP(MO, OP, DI, FU) do {                                                                            \
-        if (lake && MO == 0) launch_p<MO, OP, DI, FU, true, true, false>(m, p, Y, dy, i0, i1, cur, dg, lk, s); \
+        if (lake && MO == 0) {                                                                            \
+            if (gh) launch_p<MO, OP, DI, FU, true, true, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s);      \
+            else launch_p<MO, OP, DI, FU, true, true, false>(m, p, Y, dy, i0, i1, cur, dg, lk, s);        \
+        }                                                                                                 \
         else if (p.ncls <= LDS_CLS_MAX) {                                                                 \
             if (gh) launch_p<MO, OP, DI, FU, true, false, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s);     \
             else launch_p<MO, OP, DI, FU, true, false, false>(m, p, Y, dy, i0, i1, cur, dg, lk, s);       \

@@ -35,7 +35,7 @@ struct EtState;                           // shud_et.cpp
 struct shud_rhs {
     int NE = 0, NR = 0, NS = 0;          // local totals (incl. ghosts)
     int n_own = 0, n_segghost = 0, n_own_riv = 0;
-    bool lakeon = false;                 // lakes: any iLake > 0; serial, unpartitioned, packed
+    bool lakeon = false;                 // lakes: any iLake > 0; serial, packed
     int NL = 0;
     DevLake lk{};
     int n_int = 0;                       // partitioned: owned prefix independent of ghost data

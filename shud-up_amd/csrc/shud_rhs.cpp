@@ -64,7 +64,7 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
                         const std::vector<int> &seg_off, const std::vector<int> &up_off,
                         const std::vector<int> &up_idx);
 
-static int build_lakes(shud_rhs *h, const ShudMeshSoA *m);
+static int build_lakes(shud_rhs *h, const ShudMeshSoA *m, const ShudPartition *part);
 static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, const ShudRhsOptions *opt,
                  const ShudPartition *part) {
     const int NE = m->num_ele, NR = m->num_riv, NS = m->num_seg;
@@ -97,14 +97,15 @@ static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, cons
         if (!pp[k]) return shud_fail(SHUD_ERR_ARG, "missing parameter array #%d", k);
     for (long long q = 0; q < 3LL * NE; q++)
         if (m->nabr[q] < -1 || m->nabr[q] >= NE) return shud_fail(SHUD_ERR_ARG, "nabr[%lld]=%d out of range", q, m->nabr[q]);
-    // lakes: on when any iLake > 0 (MD_readin.cpp:262-263); serial semantics, unpartitioned, packed layout
+    // lakes: on when any iLake > 0 (MD_readin.cpp:262-263); serial semantics, packed layout.  Partitioned:
+    // the plan (shud_partition.h) puts a lake's elements and bank elements on one rank and numbers its lakes
+    // locally, so every lake sum is formed from owned elements and owned or ghost reaches
     if (m->ilake)
         for (int i = 0; i < NE; i++)
             if (m->ilake[i] > 0) h->lakeon = true;
     if (h->lakeon) {
         if (h->mode != SHUD_MODE_SERIAL)
             return shud_fail(SHUD_ERR_UNSUPPORTED, "lakes: the OMP path has no lake physics (MD_f_omp.cpp)");
-        if (part) return shud_fail(SHUD_ERR_UNSUPPORTED, "lakes: partitioned handles not supported");
         h->NL = m->num_lake;
         if (h->NL <= 0 || !m->lake_bathy_off || !m->lake_bathy_y || !m->lake_bathy_a)
             return shud_fail(SHUD_ERR_ARG, "lake elements present but no lake bathymetry (num_lake %d)", m->num_lake);
@@ -296,7 +297,7 @@ static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, cons
     }
 #undef UP
     if ((rc = build_packed(h, m, p, eflags, seg_off, up_off, up_idx))) return rc;
-    if (h->lakeon && (rc = build_lakes(h, m))) return rc;
+    if (h->lakeon && (rc = build_lakes(h, m, part))) return rc;
     if ((rc = h->dalloc(&h->d_err, 1))) return rc;
     if ((rc = h->dalloc(&h->d_warn, (size_t)kWarnSlots * kWarnStride))) return rc;
     d.err = h->d_err;
@@ -320,9 +321,11 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     if ((env && env[0] == '0') || h->variant) return 0;
     const int NE = m->num_ele;
     if (!m->rough || NE == 0) return 0;
-    // avgRough must be the reference's 0.5*(Rough_i + Rough_nabr) / Rough_i (Element.cpp:249-265)
+    // avgRough must be the reference's 0.5*(Rough_i + Rough_nabr) / Rough_i (Element.cpp:249-265).  Owned
+    // elements only: a ghost never computes lateral fluxes, and its neighbours outside the rank's local mesh
+    // appear as boundary edges (-1) while its avgRough is the global one
     for (int j = 0; j < 3; j++)
-        for (int i = 0; i < NE; i++) {
+        for (int i = 0; i < h->n_own; i++) {
             const int nb = m->nabr[(size_t)j * NE + i];
             const double want = nb >= 0 ? 0.5 * (m->rough[i] + m->rough[nb]) : m->rough[i];
             if (!(m->avg_rough[(size_t)j * NE + i] == want)) return 0;
@@ -501,18 +504,23 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
 }
 
 // Lakes: lake / bank-edge / inflow lists in the reference's summation orders, bathymetry.
-static int build_lakes(shud_rhs *h, const ShudMeshSoA *m) {
+static int build_lakes(shud_rhs *h, const ShudMeshSoA *m, const ShudPartition *part) {
     const int NE = m->num_ele, NR = m->num_riv, NL = h->NL;
+    const int NO = h->n_own;                   // lake and bank elements are owned (partition plan)
     if (!h->packed || h->variant)
         return shud_fail(SHUD_ERR_UNSUPPORTED, "lakes need the packed layout (mesh did not qualify or SHUD_RHS_PACKED=0)");
     if (h->n_classes > 128) return shud_fail(SHUD_ERR_UNSUPPORTED, "lakes: more than 128 parameter classes");
     std::vector<int> lake_of(NE, -1), ele_off(NL + 1, 0), bank_off(NL + 1, 0), rin_off(NL + 1, 0);
     std::vector<int> ele_idx, bank_pos, rin_idx;
-    for (int i = 0; i < NE; i++)
-        if (m->ilake[i] > 0) { lake_of[i] = m->ilake[i] - 1; ele_off[m->ilake[i]]++; }
+    for (int i = 0; i < NE; i++) {
+        if (m->ilake[i] <= 0) continue;
+        if (i >= NO) return shud_fail(SHUD_ERR_ARG, "lake element %d is a ghost (partition splits a lake group)", i);
+        lake_of[i] = m->ilake[i] - 1;
+        ele_off[m->ilake[i]]++;
+    }
     // bank edges: a non-lake element's edge whose neighbour is a lake element (lakenabr, MD_Lake.cpp:131-143)
     auto bank_lake = [&](int i, int j) -> int {
-        if (m->ilake[i] > 0) return -1;
+        if (i >= NO || m->ilake[i] > 0) return -1;
         const int nb = m->nabr[(size_t)j * NE + i];
         return (nb >= 0 && m->ilake[nb] > 0) ? m->ilake[nb] - 1 : -1;
     };
@@ -534,11 +542,26 @@ static int build_lakes(shud_rhs *h, const ShudMeshSoA *m) {
         for (int r = 0; r < NR; r++)
             if (m->riv_down[r] <= -4) { const int l = (-3 - m->riv_down[r]) - 1; rin_idx[fr[l]++] = r; }
     }
+    // partitioned: local order is [interior | boundary | ghosts] / [owned | ghosts], so put every lake list in
+    // global order (the single-GPU summation order, hence bit-identical sums)
+    if (part && part->ele_gid && part->riv_gid) {
+        const int32_t *eg = part->ele_gid, *rg = part->riv_gid;
+        for (int l = 0; l < NL; l++) {
+            std::sort(ele_idx.begin() + ele_off[l], ele_idx.begin() + ele_off[l + 1],
+                      [&](int a, int b) { return eg[a] < eg[b]; });
+            std::sort(bank_pos.begin() + bank_off[l], bank_pos.begin() + bank_off[l + 1], [&](int a, int b) {
+                const int ia = a % NE, ib = b % NE;                 // pos = j*NE + i: element, then edge
+                return eg[ia] != eg[ib] ? eg[ia] < eg[ib] : a / NE < b / NE;
+            });
+            std::sort(rin_idx.begin() + rin_off[l], rin_idx.begin() + rin_off[l + 1],
+                      [&](int a, int b) { return rg[a] < rg[b]; });
+        }
+    }
     for (int l = 0; l < NL; l++)
         if (ele_off[l + 1] == ele_off[l]) return shud_fail(SHUD_ERR_ARG, "lake %d has no lake element", l + 1);
     DevLake &L = h->lk;
     L.nl = NL;
-    L.y_off = 3 * NE + NR;
+    L.y_off = 3 * h->n_own + h->n_own_riv;    // [sf|us|gw|riv|lake] over owned entities
     int rc;
     int *lo, *eo, *ei, *bo, *bp, *ro, *ri, *bto;
     double *by, *ba;

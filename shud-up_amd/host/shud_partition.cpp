@@ -421,7 +421,9 @@ void recursive_bisect(const Graph &g, const std::vector<int32_t> &verts, int p0,
 // ------------------------------------------------------------------------------------------------
 // k-way greedy boundary refinement (each level of the uncoarsening)
 // ------------------------------------------------------------------------------------------------
-void kway_refine(const Graph &g, int k, double ub, int passes, std::vector<int32_t> &part) {
+// locked (optional): vertices that stay where they are (lake groups)
+void kway_refine(const Graph &g, int k, double ub, int passes, std::vector<int32_t> &part,
+                 const std::vector<char> *locked = nullptr) {
     const int n = g.n;
     std::vector<int64_t> pw(k, 0);
     for (int v = 0; v < n; v++) pw[part[v]] += g.vw[v];
@@ -432,6 +434,7 @@ void kway_refine(const Graph &g, int k, double ub, int passes, std::vector<int32
     for (int pass = 0; pass < passes; pass++) {
         int64_t moved = 0;
         for (int v = 0; v < n; v++) {
+            if (locked && (*locked)[v]) continue;
             const int from = part[v];
             bool bnd = false;
             for (int64_t e = g.xadj[v]; e < g.xadj[v + 1]; e++)
@@ -517,7 +520,73 @@ void rcb_rec(const double *x, const double *y, const std::vector<double> &w, std
     rcb_rec(x, y, w, std::move(R), p0 + nl, np - nl, part);
 }
 
-// reach owners: the part owning most of a reach's segments' elements (lowest on ties), part 0 without segments
+// ---- lakes ----
+bool has_lakes(const ShudMeshSoA *m) { return m->num_lake > 0 && m->ilake; }
+
+// lake groups: lakes joined when elements of two lakes share an edge or a bank element (a non-lake element
+// with an edge on a lake element) touches both; grp[i] = the group's smallest lake id for lake and bank
+// elements, -1 elsewhere
+std::vector<int32_t> lake_groups(const ShudMeshSoA *m) {
+    const int NE = m->num_ele, NL = m->num_lake;
+    std::vector<int32_t> uf(NL), grp(NE, -1), first(NE, -1);
+    std::iota(uf.begin(), uf.end(), 0);
+    auto find = [&](int a) {
+        while (uf[a] != a) a = uf[a] = uf[uf[a]];
+        return a;
+    };
+    auto unite = [&](int a, int b) {
+        a = find(a);
+        b = find(b);
+        if (a != b) uf[std::max(a, b)] = std::min(a, b);
+    };
+    for (int i = 0; i < NE; i++) {
+        const int li = m->ilake[i] - 1;
+        for (int j = 0; j < 3; j++) {
+            const int nb = m->nabr[(size_t)j * NE + i];
+            if (nb < 0 || m->ilake[nb] <= 0) continue;
+            const int lj = m->ilake[nb] - 1;
+            if (li >= 0) unite(li, lj);
+            else if (first[i] < 0) first[i] = lj;
+            else unite(first[i], lj);
+        }
+    }
+    for (int i = 0; i < NE; i++) {
+        const int li = m->ilake[i] - 1;
+        if (li >= 0) grp[i] = find(li);
+        else if (first[i] >= 0) grp[i] = find(first[i]);
+    }
+    return grp;
+}
+
+// part of each lake (its elements' part; -1 for a lake without elements)
+std::vector<int32_t> lake_parts(const ShudMeshSoA *m, const int32_t *ele_part) {
+    std::vector<int32_t> lp(has_lakes(m) ? m->num_lake : 0, -1);
+    if (lp.empty()) return lp;
+    for (int i = 0; i < m->num_ele; i++)
+        if (m->ilake[i] > 0) lp[m->ilake[i] - 1] = ele_part[i];
+    return lp;
+}
+
+// move every lake group to the part holding most of its vertex weight (1 + #segments; lowest part on ties)
+void constrain_lakes(const ShudMeshSoA *m, int nparts, int32_t *ele_part) {
+    if (!has_lakes(m)) return;
+    const int NE = m->num_ele, NL = m->num_lake;
+    const std::vector<int32_t> grp = lake_groups(m);
+    std::vector<int64_t> vw(NE, 1), w((size_t)NL * nparts, 0);
+    for (int s = 0; s < m->num_seg; s++) vw[m->seg_ele[s]]++;
+    for (int i = 0; i < NE; i++)
+        if (grp[i] >= 0) w[(size_t)grp[i] * nparts + ele_part[i]] += vw[i];
+    std::vector<int32_t> best(NL, 0);
+    for (int g = 0; g < NL; g++)
+        for (int p = 1; p < nparts; p++)
+            if (w[(size_t)g * nparts + p] > w[(size_t)g * nparts + best[g]]) best[g] = p;
+    for (int i = 0; i < NE; i++)
+        if (grp[i] >= 0) ele_part[i] = best[grp[i]];
+}
+
+// reach owners: the part owning most of a reach's segments' elements (lowest on ties), part 0 without segments;
+// with lakes, a reach with a segment on a lake element belongs to that lake's part (so lake elements are never
+// segment ghosts of another rank)
 std::vector<int32_t> reach_owners(const ShudMeshSoA *m, const int32_t *ele_part, int nparts) {
     const int NR = m->num_riv;
     std::vector<int32_t> cnt((size_t)NR * nparts, 0);
@@ -529,7 +598,34 @@ std::vector<int32_t> reach_owners(const ShudMeshSoA *m, const int32_t *ele_part,
             if (cnt[(size_t)r * nparts + p] > cnt[(size_t)r * nparts + best]) best = p;
         rp[r] = best;
     }
+    if (has_lakes(m))
+        for (int s = 0; s < m->num_seg; s++)
+            if (m->ilake[m->seg_ele[s]] > 0) rp[m->seg_riv[s]] = ele_part[m->seg_ele[s]];
     return rp;
+}
+
+// a plan with lakes needs every lake group on one part and every lake element's segments owned there
+int check_lake_partition(const ShudMeshSoA *m, const int32_t *ele_part, const std::vector<int32_t> &rp) {
+    if (!has_lakes(m)) return 0;
+    const int NE = m->num_ele;
+    const std::vector<int32_t> lp = lake_parts(m, ele_part);
+    for (int i = 0; i < NE; i++) {
+        if (m->ilake[i] <= 0) continue;
+        if (ele_part[i] != lp[m->ilake[i] - 1])
+            return perr(SHUD_ERR_UNSUPPORTED, "lake %d is split across parts (shud_partition_constrain)", m->ilake[i]);
+        for (int j = 0; j < 3; j++) {
+            const int nb = m->nabr[(size_t)j * NE + i];
+            if (nb >= 0 && ele_part[nb] != ele_part[i])
+                return perr(SHUD_ERR_UNSUPPORTED, "lake element %d and its neighbour %d lie on different parts "
+                            "(shud_partition_constrain)", i, nb);
+        }
+    }
+    for (int s = 0; s < m->num_seg; s++) {
+        const int e = m->seg_ele[s];
+        if (m->ilake[e] > 0 && rp[m->seg_riv[s]] != ele_part[e])
+            return perr(SHUD_ERR_UNSUPPORTED, "reach %d has segments on lake elements of different parts", m->seg_riv[s]);
+    }
+    return 0;
 }
 
 void mesh_cuts(const ShudMeshSoA *m, const int32_t *ele_part, int nparts, int64_t *ec, int64_t *sc) {
@@ -571,12 +667,16 @@ void need_masks(const ShudMeshSoA *m, const int32_t *ele_part, const std::vector
         ne[e] |= b;
         nr[r] |= b;
     }
+    const std::vector<int32_t> lp = lake_parts(m, ele_part);
     for (int r = 0; r < NR; r++) {
         nr[r] |= 1ull << rp[r];
         const int d = m->riv_down[r];
         if (d >= 0) {
             nr[d] |= 1ull << rp[r];          // downstream of an owned reach
             nr[r] |= 1ull << rp[d];          // upstream of an owned reach
+        } else if (d <= -4 && !lp.empty()) {
+            const int L = -3 - d - 1;        // flows into lake L: its QrivDown is summed by the lake's owner
+            if (L < (int)lp.size() && lp[L] >= 0) nr[r] |= 1ull << lp[L];
         }
     }
 }
@@ -613,6 +713,9 @@ int check_mesh(const ShudMeshSoA *m) {
         if (m->nabr[k] >= m->num_ele) return perr(SHUD_ERR_ARG, "nabr out of range");
     for (int r = 0; r < m->num_riv; r++)
         if (m->riv_down && m->riv_down[r] >= m->num_riv) return perr(SHUD_ERR_ARG, "riv_down out of range");
+    if (has_lakes(m))
+        for (int i = 0; i < m->num_ele; i++)
+            if (m->ilake[i] < 0 || m->ilake[i] > m->num_lake) return perr(SHUD_ERR_ARG, "ilake[%d] out of range", i);
     return 0;
 }
 
@@ -622,6 +725,16 @@ int check_mesh(const ShudMeshSoA *m) {
 // partitioner
 // ================================================================================================
 extern "C" const char *shud_partition_error(void) { return g_err.c_str(); }
+
+extern "C" int shud_partition_constrain(const ShudMeshSoA *mesh, int32_t nparts, int32_t *ele_part) {
+    int rc = check_mesh(mesh);
+    if (rc) return rc;
+    if (!ele_part || nparts < 1 || nparts > SHUD_PART_MAX_PARTS) return perr(SHUD_ERR_ARG, "bad partition");
+    for (int i = 0; i < mesh->num_ele; i++)
+        if (ele_part[i] < 0 || ele_part[i] >= nparts) return perr(SHUD_ERR_ARG, "ele_part[%d] out of range", i);
+    constrain_lakes(mesh, nparts, ele_part);
+    return 0;
+}
 
 extern "C" int shud_partition_cut(const ShudMeshSoA *mesh, const int32_t *ele_part, int32_t nparts, int64_t *ec,
                                   int64_t *sc) {
@@ -665,6 +778,14 @@ static int partition_one(const ShudMeshSoA *mesh, const double *cx, const double
         lap("recursive bisection");
         kway_refine(g, nparts, ub, 8, part);                    // k-way polish of the assembled partition
         lap("k-way refinement");
+        if (has_lakes(mesh)) {
+            // lake groups onto one part each, then rebalance around them (group vertices locked)
+            constrain_lakes(mesh, nparts, part.data());
+            const std::vector<int32_t> grp = lake_groups(mesh);
+            std::vector<char> locked(NE, 0);
+            for (int i = 0; i < NE; i++) locked[i] = grp[i] >= 0;
+            kway_refine(g, nparts, ub, 16, part, &locked);
+        }
         S.levels = levels;
         S.coarse_vertices = coarse_n;
         S.graph_cut = graph_cut(g, part);
@@ -672,6 +793,7 @@ static int partition_one(const ShudMeshSoA *mesh, const double *cx, const double
     } else {
         return perr(SHUD_ERR_ARG, "unknown method %d", method);
     }
+    constrain_lakes(mesh, nparts, ele_part);                    // lake groups on one part each
     // every part must own at least one element
     std::vector<int64_t> pw(nparts, 0), pn(nparts, 0);
     int64_t tw = 0;
@@ -738,6 +860,10 @@ struct shud_plan {
     std::vector<int32_t> ele_gid, riv_gid, seg_gid;      // local -> global
     int n_own_ele = 0, n_int = 0, n_own_riv = 0;
     std::vector<int32_t> riv_part;
+    int NLg = 0;
+    std::vector<int32_t> lake_gid;                        // owned lakes (0-based global ids), ascending
+    std::vector<int32_t> l_bathy_off;
+    std::vector<double> l_bathy_y, l_bathy_a;
     std::vector<int32_t> esend_off, esend_idx, erecv_off, rsend_off, rsend_idx, rrecv_off;
     // local mesh storage (shud_plan_local_mesh)
     std::vector<double> d_ele1[5], d_ele3[4], d_riv[9], d_seg[2], d_par[17];
@@ -750,17 +876,24 @@ extern "C" int shud_plan_build(const ShudMeshSoA *m, const int32_t *ele_part, in
     if (rc) return rc;
     if (!out || !ele_part || nparts < 1 || nparts > SHUD_PART_MAX_PARTS || rank < 0 || rank >= nparts)
         return perr(SHUD_ERR_ARG, "bad plan arguments");
-    if (m->num_lake > 0) return perr(SHUD_ERR_UNSUPPORTED, "lakes are not supported in partitioned handles");
     const int NE = m->num_ele, NR = m->num_riv, NS = m->num_seg;
     for (int i = 0; i < NE; i++)
         if (ele_part[i] < 0 || ele_part[i] >= nparts) return perr(SHUD_ERR_ARG, "ele_part[%d] out of range", i);
+    std::vector<int32_t> rp0 = reach_owners(m, ele_part, nparts);
+    if ((rc = check_lake_partition(m, ele_part, rp0))) return rc;
     auto *P = new shud_plan;
     P->rank = rank;
     P->nparts = nparts;
     P->NEg = NE;
     P->NRg = NR;
-    P->riv_part = reach_owners(m, ele_part, nparts);
+    P->riv_part = std::move(rp0);
     const std::vector<int32_t> &rp = P->riv_part;
+    if (has_lakes(m)) {
+        P->NLg = m->num_lake;
+        const std::vector<int32_t> lp = lake_parts(m, ele_part);
+        for (int l = 0; l < m->num_lake; l++)
+            if (lp[l] == rank) P->lake_gid.push_back(l);
+    }
     std::vector<uint64_t> ne, nr;
     need_masks(m, ele_part, rp, ne, nr);
     const uint64_t me = 1ull << rank;
@@ -847,6 +980,8 @@ extern "C" int shud_plan_info(shud_plan_t p, ShudPlanInfo *I) {
     I->riv_gid = p->riv_gid.data();
     I->seg_gid = p->seg_gid.data();
     I->riv_part = p->riv_part.data();
+    I->n_own_lake = (int32_t)p->lake_gid.size();
+    I->lake_gid = p->lake_gid.data();
     return 0;
 }
 
@@ -873,7 +1008,8 @@ extern "C" int shud_plan_local_mesh(shud_plan_t p, const ShudMeshSoA *g, const S
                                     ShudParamsSoA *lp) {
     if (!p || !g || !gp || !L || !lp) return perr(SHUD_ERR_ARG, "null argument");
     if (g->num_ele != p->NEg || g->num_riv != p->NRg) return perr(SHUD_ERR_ARG, "mesh does not match the plan");
-    if (g->num_lake > 0) return perr(SHUD_ERR_UNSUPPORTED, "lakes are not supported in partitioned handles");
+    if (has_lakes(g) != (p->NLg > 0) || (p->NLg > 0 && g->num_lake != p->NLg))
+        return perr(SHUD_ERR_ARG, "mesh lakes do not match the plan");
     const int NEg = g->num_ele;
     const int NEl = (int)p->ele_gid.size(), NRl = (int)p->riv_gid.size(), NSl = (int)p->seg_gid.size();
     const std::vector<int32_t> &le = p->ele_gid, &lr = p->riv_gid, &ls = p->seg_gid;
@@ -929,10 +1065,44 @@ extern "C" int shud_plan_local_mesh(shud_plan_t p, const ShudMeshSoA *g, const S
     L->ibc = gati(g->ibc, p->l_ibc, le);
     L->iss = gati(g->iss, p->l_iss, le);
     L->ilake = gati(g->ilake, p->l_ilake, le);
+    // lakes: owned lakes renumbered 1..n_own_lake (lake elements are always owned, check_lake_partition)
+    std::vector<int32_t> g2ll(p->NLg, -1);
+    for (size_t k = 0; k < p->lake_gid.size(); k++) g2ll[p->lake_gid[k]] = (int32_t)k;
+    if (p->NLg > 0) {
+        for (int k = 0; k < NEl; k++) {
+            const int v = p->l_ilake[k];
+            if (v <= 0) continue;
+            if (g2ll[v - 1] < 0) return perr(SHUD_ERR_ARG, "element %d of lake %d is local but the lake is not owned", le[k], v);
+            p->l_ilake[k] = g2ll[v - 1] + 1;
+        }
+        const int nl = (int)p->lake_gid.size();
+        p->l_bathy_off.assign(1, 0);
+        p->l_bathy_y.clear();
+        p->l_bathy_a.clear();
+        for (int k = 0; k < nl; k++) {
+            const int l = p->lake_gid[k];
+            for (int q = g->lake_bathy_off[l]; q < g->lake_bathy_off[l + 1]; q++) {
+                p->l_bathy_y.push_back(g->lake_bathy_y[q]);
+                p->l_bathy_a.push_back(g->lake_bathy_a[q]);
+            }
+            p->l_bathy_off.push_back((int32_t)p->l_bathy_y.size());
+        }
+        L->num_lake = nl;
+        L->lake_bathy_off = nl ? p->l_bathy_off.data() : nullptr;
+        L->lake_bathy_y = nl ? p->l_bathy_y.data() : nullptr;
+        L->lake_bathy_a = nl ? p->l_bathy_a.data() : nullptr;
+    }
     p->l_down.resize(NRl);
     for (int k = 0; k < NRl; k++) {
         const int d = g->riv_down[lr[k]];
-        p->l_down[k] = d >= 0 ? (g2lr[d] >= 0 ? g2lr[d] : -3) : d;
+        if (d >= 0) {
+            p->l_down[k] = g2lr[d] >= 0 ? g2lr[d] : -3;
+        } else if (d <= -4 && p->NLg > 0) {            // into lake -3 - d: local id if owned, else the outlet code
+            const int l = g2ll[-3 - d - 1];
+            p->l_down[k] = l >= 0 ? -3 - (l + 1) : -3;
+        } else {
+            p->l_down[k] = d;
+        }
     }
     L->riv_down = p->l_down.data();
     L->riv_bc = gati(g->riv_bc, p->l_rbc, lr);
@@ -985,6 +1155,8 @@ extern "C" int shud_plan_owned_state(shud_plan_t p, const double *y, int32_t neg
     for (int b = 0; b < 3; b++)
         for (int k = 0; k < no; k++) o[(size_t)b * no + k] = y[(size_t)b * neg + p->ele_gid[k]];
     for (int k = 0; k < nro; k++) o[3 * (size_t)no + k] = y[3 * (size_t)neg + p->riv_gid[k]];
+    for (size_t k = 0; k < p->lake_gid.size(); k++)
+        o[3 * (size_t)no + nro + k] = y[3 * (size_t)neg + p->NRg + p->lake_gid[k]];
     return 0;
 }
 
@@ -994,5 +1166,7 @@ extern "C" int shud_plan_scatter_owned(shud_plan_t p, const double *o, int32_t n
     for (int b = 0; b < 3; b++)
         for (int k = 0; k < no; k++) y[(size_t)b * neg + p->ele_gid[k]] = o[(size_t)b * no + k];
     for (int k = 0; k < nro; k++) y[3 * (size_t)neg + p->riv_gid[k]] = o[3 * (size_t)no + k];
+    for (size_t k = 0; k < p->lake_gid.size(); k++)
+        y[3 * (size_t)neg + p->NRg + p->lake_gid[k]] = o[3 * (size_t)no + nro + k];
     return 0;
 }

@@ -83,11 +83,16 @@ class LocalPartition:
     riv_recv_off: np.ndarray
     seg_gid: np.ndarray
     nccl_unique_id: bytes = None
+    lake_gid: np.ndarray = None            # owned lakes (0-based global ids), C++ plans only
     _keep: List = field(default_factory=list)
 
     @property
     def n_segghost_ele(self):
         return self.ele_gid.size - self.n_own_ele
+
+    @property
+    def n_own_lake(self):
+        return 0 if self.lake_gid is None else int(self.lake_gid.size)
 
     def struct(self):
         p = abi.ShudPartition()
@@ -236,11 +241,13 @@ def local_model(m, plan, rank, nranks):
 
 
 def local_state(y_global, m_global, part):
-    """Owned part of a global state vector in the rank's reference block layout."""
-    NE = m_global.num_ele
+    """Owned part of a global state vector in the rank's reference block layout [sf|us|gw|riv|lake]."""
+    NE, NR = m_global.num_ele, m_global.num_riv
     oe = part.ele_gid[:part.n_own_ele]
     orr = part.riv_gid[:part.n_own_riv]
-    return np.concatenate([y_global[oe], y_global[NE + oe], y_global[2 * NE + oe], y_global[3 * NE + orr]])
+    ol = part.lake_gid if part.lake_gid is not None else np.zeros(0, np.int64)
+    return np.concatenate([y_global[oe], y_global[NE + oe], y_global[2 * NE + oe], y_global[3 * NE + orr],
+                           y_global[3 * NE + NR + ol]])
 
 
 def ghost_values(y_global, m_global, part):
@@ -253,21 +260,22 @@ def ghost_values(y_global, m_global, part):
 
 
 def extended_state(y_owned, gele, griv, part):
-    """[sf|us|gw|riv] over ALL local entities (owned + ghost): the CPU oracle's input for a rank."""
-    no, nro = part.n_own_ele, part.n_own_riv
+    """[sf|us|gw|riv|lake] over ALL local entities (owned + ghost; lakes are always owned): the CPU oracle's
+    input for a rank."""
+    no, nro, nl = part.n_own_ele, part.n_own_riv, part.n_own_lake
     g = gele.reshape(-1, 3)
     sf = np.concatenate([y_owned[:no], g[:, 0]])
     us = np.concatenate([y_owned[no:2 * no], g[:, 1]])
     gw = np.concatenate([y_owned[2 * no:3 * no], g[:, 2]])
     rv = np.concatenate([y_owned[3 * no:3 * no + nro], griv])
-    return np.concatenate([sf, us, gw, rv])
+    return np.concatenate([sf, us, gw, rv, y_owned[3 * no + nro:3 * no + nro + nl]])
 
 
 def owned_dy(dy_ext, lm, part):
     """Owned entries of an extended-layout ydot, in the owned block layout."""
-    NEl, no, nro = lm.num_ele, part.n_own_ele, part.n_own_riv
+    NEl, NRl, no, nro, nl = lm.num_ele, lm.num_riv, part.n_own_ele, part.n_own_riv, part.n_own_lake
     return np.concatenate([dy_ext[:no], dy_ext[NEl:NEl + no], dy_ext[2 * NEl:2 * NEl + no],
-                           dy_ext[3 * NEl:3 * NEl + nro]])
+                           dy_ext[3 * NEl:3 * NEl + nro], dy_ext[3 * NEl + NRl:3 * NEl + NRl + nl]])
 
 
 def pack_send(y_owned, part):
@@ -296,7 +304,8 @@ class ShudPlanInfo(C.Structure):
     _fields_ = [("n_own_ele", C.c_int32), ("n_int_ele", C.c_int32), ("n_ghost_ele", C.c_int32),
                 ("n_own_riv", C.c_int32), ("n_ghost_riv", C.c_int32), ("n_seg", C.c_int32),
                 ("ele_gid", C.POINTER(C.c_int32)), ("riv_gid", C.POINTER(C.c_int32)),
-                ("seg_gid", C.POINTER(C.c_int32)), ("riv_part", C.POINTER(C.c_int32))]
+                ("seg_gid", C.POINTER(C.c_int32)), ("riv_part", C.POINTER(C.c_int32)),
+                ("n_own_lake", C.c_int32), ("lake_gid", C.POINTER(C.c_int32))]
 
 
 _HL = None
@@ -311,6 +320,7 @@ def _host():
         sig = {
             "shud_partition_mesh": (C.c_int, [C.POINTER(abi.ShudMeshSoA), C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
                                               C.c_uint64, C.c_void_p, C.POINTER(ShudPartStats)]),
+            "shud_partition_constrain": (C.c_int, [C.POINTER(abi.ShudMeshSoA), C.c_int32, C.c_void_p]),
             "shud_partition_cut": (C.c_int, [C.POINTER(abi.ShudMeshSoA), C.c_void_p, C.c_int32,
                                              C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
             "shud_partition_halo": (C.c_int, [C.POINTER(abi.ShudMeshSoA), C.c_void_p, C.c_int32, C.c_void_p,
@@ -353,6 +363,14 @@ def cpp_partition(m, nparts, method=PART_MULTILEVEL, seed=12345):
                                         int(seed), part.ctypes.data, C.byref(st)), "shud_partition_mesh")
     stats = {k: getattr(st, k) for k, _ in ShudPartStats._fields_}
     return part, stats
+
+
+def cpp_constrain(m, ele_part, nparts):
+    """A caller's partition with every lake group moved onto one part (shud_partition_constrain)."""
+    ms = m.mesh_struct()
+    ep = np.array(ele_part, dtype=np.int32)
+    _hcheck(_host().shud_partition_constrain(C.byref(ms), int(nparts), ep.ctypes.data), "shud_partition_constrain")
+    return ep
 
 
 def cpp_edge_cut(m, ele_part):
@@ -398,6 +416,8 @@ class CppPlan:
                         else np.zeros(0, np.int32))
         self.riv_part = (np.ctypeslib.as_array(info.riv_part, shape=(m.num_riv,)).copy() if m.num_riv
                          else np.zeros(0, np.int32))
+        self.lake_gid = (np.ctypeslib.as_array(info.lake_gid, shape=(info.n_own_lake,)).copy() if info.n_own_lake
+                         else np.zeros(0, np.int32))
         sp = abi.ShudPartition()
         _hcheck(_host().shud_plan_partition(h, C.byref(sp)), "shud_plan_partition")
         P = nparts + 1
@@ -427,7 +447,7 @@ class CppPlan:
                               ele_gid=self.ele_gid, riv_gid=self.riv_gid, ele_send_off=self.ele_send_off,
                               ele_send_idx=self.ele_send_idx, ele_recv_off=self.ele_recv_off,
                               riv_send_off=self.riv_send_off, riv_send_idx=self.riv_send_idx,
-                              riv_recv_off=self.riv_recv_off, seg_gid=self.seg_gid)
+                              riv_recv_off=self.riv_recv_off, seg_gid=self.seg_gid, lake_gid=self.lake_gid)
 
     def gather_ele(self, a):
         a = np.ascontiguousarray(a, dtype=np.float64)
@@ -437,7 +457,7 @@ class CppPlan:
 
     def owned_state(self, y):
         y = np.ascontiguousarray(y, dtype=np.float64)
-        out = np.empty(3 * self.n_own_ele + self.n_own_riv)
+        out = np.empty(3 * self.n_own_ele + self.n_own_riv + self.lake_gid.size)
         _hcheck(_host().shud_plan_owned_state(self.h, y.ctypes.data, self.m.num_ele, out.ctypes.data),
                 "shud_plan_owned_state")
         return out
@@ -465,6 +485,12 @@ class CppPlan:
         lm.nabr = d(lms.nabr, 3 * NE)
         lm.ibc, lm.iss = d(lms.ibc, NE), d(lms.iss, NE)
         lm.ilake = d(lms.ilake, NE)
+        if lms.num_lake > 0:
+            nl = lms.num_lake
+            lm.num_lake = nl
+            lm.lake_bathy_off = d(lms.lake_bathy_off, nl + 1)
+            nb = int(lm.lake_bathy_off[-1])
+            lm.lake_bathy_y, lm.lake_bathy_a = d(lms.lake_bathy_y, nb), d(lms.lake_bathy_a, nb)
         for k in RIV_D:
             v = d(getattr(lms, k), NR)
             lm.riv[k] = v if v is not None else np.zeros(NR)

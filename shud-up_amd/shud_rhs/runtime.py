@@ -57,7 +57,7 @@ class RhsHandle:
                                                      C.byref(self._part), C.byref(h)),
                    "shud_rhs_create_partitioned")
             self.n_own, self.n_own_riv = partition.n_own_ele, partition.n_own_riv
-            self.n_lake = 0                             # lakes: unpartitioned handles only
+            self.n_lake = getattr(model, "num_lake", 0)   # the local mesh carries the owned lakes
         self.h = h
         self.mode = mode
 

@@ -28,9 +28,12 @@ def _run_ranks(m, y_list, locs, mode, ncalls=3):
     try:
         for lm, part in locs:
             h = rt.RhsHandle(lm, mode=mode, partition=part)
+            # a local mesh takes the same kernel layout as the whole mesh (ghosts' boundary-looking edges must
+            # not push a rank onto the SoA kernel)
+            assert h.layout()["packed"] == single.layout()["packed"], (h.layout(), single.layout())
             h.set_step_inputs()
             hs.append(h)
-            ny = 3 * part.n_own_ele + part.n_own_riv
+            ny = 3 * part.n_own_ele + part.n_own_riv + part.n_own_lake
             bufs.append((h.device_alloc(8 * ny), h.device_alloc(8 * ny), ny))
             halos.append(h.halo_buffers())
         for yy in y_list:
@@ -107,6 +110,29 @@ def test_ragged_random_partitions(nranks, seed):
     locs = [partition.CppPlan(m, ep, nranks, r).local_model() for r in range(nranks)]
     for mode in (0, 1):
         _run_ranks(m, [y, workload.random_state(m, seed=seed + 1)], locs, mode, ncalls=2)
+
+
+@pytest.mark.parametrize("case", ["qhh", "qhh_variant"])
+@pytest.mark.parametrize("nranks", [2, 3, 4])
+def test_lake_partitions_bit_identical(case, nranks):
+    """Lakes in partitioned handles: the C++ partitioner keeps each lake group (lake + bank
+    elements) on one rank, which owns the lake stage and sums its terms in global order; reaches flowing into
+    the lake (qhh_variant) are ghosts there when owned elsewhere.  Owned DY, lake stages included, must equal
+    the single-GPU handle's bit for bit."""
+    m, y = getattr(cases, case)()
+    ep, _ = partition.cpp_partition(m, nranks, partition.PART_MULTILEVEL)
+    locs = [partition.CppPlan(m, ep, nranks, r).local_model() for r in range(nranks)]
+    assert sum(p.n_own_lake for _, p in locs) == m.num_lake
+    _run_ranks(m, [y, workload.random_state(m, seed=3)], locs, 0, ncalls=2)
+
+
+def test_lake_random_constrained_partition():
+    """A ragged random partition of qhh_variant made lake-consistent by shud_partition_constrain."""
+    m, y = cases.qhh_variant()
+    rng = np.random.default_rng(11)
+    ep = partition.cpp_constrain(m, rng.integers(0, 4, m.num_ele).astype(np.int32), 4)
+    locs = [partition.CppPlan(m, ep, 4, r).local_model() for r in range(4)]
+    _run_ranks(m, [y], locs, 0, ncalls=2)
 
 
 @pytest.mark.parametrize("nranks", [2, 8])

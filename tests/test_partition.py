@@ -285,3 +285,58 @@ def test_multilevel_beats_rcb_on_bisection():
     _, ml = partition.cpp_partition(m, 2, partition.PART_MULTILEVEL)
     _, rcb = partition.cpp_partition(m, 2, partition.PART_RCB)
     assert ml["edge_cut"] < rcb["edge_cut"] and ml["segment_cut"] < rcb["segment_cut"]
+
+
+@pytest.mark.parametrize("case", ["qhh", "qhh_variant"])
+@pytest.mark.parametrize("nparts", [2, 3, 4, 8])
+def test_lake_plans(case, nparts):
+    """Lakes in C++ plans: every lake group (lake elements + bank elements) on one part, each lake owned by
+    exactly one rank with its inflowing reaches local there, owned-state round trip with lake stages, local
+    lake numbering, balance kept around the locked groups."""
+    m, y = getattr(cases, case)()
+    ep, st = partition.cpp_partition(m, nparts, partition.PART_MULTILEVEL)
+    nab = m.nabr.reshape(3, -1)
+    lk = np.nonzero(m.ilake > 0)[0]
+    for j in range(3):
+        nb = nab[j, lk]
+        assert np.all(ep[nb[nb >= 0]] == ep[lk[nb >= 0]])
+    assert st["imbalance"] < 1.06
+    plans = [partition.CppPlan(m, ep, nparts, r) for r in range(nparts)]
+    assert np.array_equal(np.sort(np.concatenate([p.lake_gid for p in plans])), np.arange(m.num_lake))
+    y2 = np.zeros_like(y)
+    for p in plans:
+        o = p.owned_state(y)
+        assert o.size == 3 * p.n_own_ele + p.n_own_riv + p.lake_gid.size
+        partition._host().shud_plan_scatter_owned(p.h, o.ctypes.data, m.num_ele, y2.ctypes.data)
+    assert np.array_equal(y, y2)
+    for r, p in enumerate(plans):
+        lm, part = p.local_model()
+        assert lm.num_lake == part.n_own_lake == p.lake_gid.size
+        li = lm.ilake
+        assert np.all((li >= 0) & (li <= lm.num_lake))
+        assert np.all(np.nonzero(li > 0)[0] < part.n_own_ele)          # lake elements are owned
+        for k, gl in enumerate(p.lake_gid):                             # inflowing reaches are local
+            inflow = np.nonzero(m.riv_down == -3 - (gl + 1))[0]
+            assert np.isin(inflow, p.riv_gid).all()
+            loc = np.nonzero(np.isin(p.riv_gid, inflow))[0]
+            assert np.all(lm.riv_down[loc] == -3 - (k + 1))
+        others = np.nonzero((m.riv_down <= -4) & ~np.isin(-3 - m.riv_down - 1, p.lake_gid))[0]
+        assert np.all(lm.riv_down[np.isin(p.riv_gid, others)] == -3)  # into a lake owned elsewhere: outlet code
+        p.close()
+
+
+def test_lake_partition_constraint():
+    m, _ = cases.qhh_variant()
+    rng = np.random.default_rng(5)
+    ep = rng.integers(0, 4, m.num_ele).astype(np.int32)
+    with pytest.raises(RuntimeError, match="lake"):
+        partition.CppPlan(m, ep, 4, 0)
+    ec = partition.cpp_constrain(m, ep, 4)
+    assert np.array_equal(partition.cpp_constrain(m, ec, 4), ec)            # idempotent
+    moved = np.nonzero(ec != ep)[0]
+    assert np.all((m.ilake[moved] > 0) | np.isin(moved, m.nabr.reshape(3, -1)[:, m.ilake > 0]))
+    for r in range(4):
+        partition.CppPlan(m, ec, 4, r).close()
+    m2, _ = cases.variant(3000, seed=4)                                     # no lakes: untouched
+    ep2 = rng.integers(0, 3, m2.num_ele).astype(np.int32)
+    assert np.array_equal(partition.cpp_constrain(m2, ep2, 3), ep2)
