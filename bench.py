@@ -87,9 +87,20 @@ def main():
     stream = torch.cuda.current_stream()
     if world > 1 or args.partition_1:
         # the C++ partitioner + planner (include/shud_partition.h): multilevel and RCB, the smaller largest
-        # halo wins; every rank computes the same partition (deterministic), then only its own plan
+        # halo wins; rank 0 partitions (deterministic: any rank would get the same parts) and broadcasts the
+        # element -> part map, then every rank builds only its own plan
         tp = time.time()
-        ele_part, pst = partition.cpp_partition(gm, world, partition.PART_AUTO, seed=12345)
+        if rank == 0:
+            ele_part, pst = partition.cpp_partition(gm, world, partition.PART_AUTO, seed=12345)
+        else:
+            ele_part, pst = np.zeros(gm.num_ele, np.int32), None
+        if world > 1:
+            ep_t = torch.from_numpy(ele_part).to(f"cuda:{local}")
+            dist.broadcast(ep_t, src=0)
+            ele_part = ep_t.cpu().numpy()
+            box = [pst]
+            dist.broadcast_object_list(box, src=0)
+            pst = box[0]
         cut_e, cut_s = pst["edge_cut"], pst["segment_cut"]
         plan = partition.CppPlan(gm, ele_part, world, rank)
         lm, part = plan.local_model()
