@@ -725,6 +725,9 @@ extern "C" int shud_rhs_set_step_inputs(shud_rhs_t h, const ShudStepInputs *in) 
 // ev_comm marks the ghost buffers filled.
 static int exchange(shud_rhs *h, const double *y) {
     if (!h->partitioned) return 0;
+    // SHUD_RHS_NOPACK=1: timing ablation for external transport only (tools/rank_timing.py): no pack kernel
+    static const bool nopack = [] { const char *e = getenv("SHUD_RHS_NOPACK"); return e && e[0] == '1'; }();
+    if (nopack && !h->use_nccl) return 0;
     launch_pack_kernel(y, h->n_own, h->n_own_riv, h->d_esend_idx, h->n_esend, h->d_rsend_idx, h->n_rsend,
                        h->d_esend, h->d_rsend, h->stream);
     if (!h->use_nccl) return 0;      // external transport (tests): caller moved the buffers
@@ -794,7 +797,9 @@ static const uint32_t kFatal = SHUD_EF_NAN_QELE | SHUD_EF_EFFKH | SHUD_EF_ET_NEG
 // partitioned handles: the interior elements [0, n_int) run while the halo exchange is in flight (RCCL on
 // s_comm); boundary + ghost elements and the reaches wait for it.  Unpartitioned: one launch each.
 static int launch_split(shud_rhs *h, const double *y, double *dy, hipEvent_t e_mid = nullptr) {
-    if (h->partitioned && h->packed && !h->variant && h->n_int > 0) {
+    // SHUD_RHS_NOSPLIT=1: timing ablation (tools/rank_timing.py): one element launch after the exchange
+    static const bool nosplit = [] { const char *e = getenv("SHUD_RHS_NOSPLIT"); return e && e[0] == '1'; }();
+    if (h->partitioned && h->packed && !h->variant && h->n_int > 0 && !nosplit) {
         launch_ele(h, y, dy, h->cur, h->cur_e, false, 0, h->n_int);
         if (h->use_nccl) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_comm, 0));
         launch_ele(h, y, dy, h->cur, h->cur_e, false, h->n_int, h->n_own + h->n_segghost);
