@@ -232,6 +232,9 @@ def main():
         out["roofline"].update(tr)
         if out["roofline"].get("traffic"):
             out["roofline"]["frac_actual"] = out["roofline"]["traffic"] / (ms_ele * 1e-3) / HBM_PEAK
+            if sp:   # measured bytes against the measured copy ceiling (the canonical count exceeds the bytes moved)
+                out["roofline"]["frac_of_stream_copy_actual"] = (out["roofline"]["traffic"] / (ms_ele * 1e-3) / 1e9
+                                                                 / sp["stream_copy_GBs"])
         rt = tr.get("riv_traffic")
         if rt and ms_riv > 0:
             out["roofline"]["riv_frac_actual"] = rt / (ms_riv * 1e-3) / HBM_PEAK
