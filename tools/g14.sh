@@ -1,3 +1,4 @@
+# GPU box: full GPU suite, then the round profile (tools/profile_round.sh).
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/g14

@@ -1,3 +1,4 @@
+# GPU box: full GPU suite (edge meshes, ragged partitions) and the driver bench command.
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/g16
