@@ -135,15 +135,16 @@ def test_lake_random_constrained_partition():
     _run_ranks(m, [y], locs, 0, ncalls=2)
 
 
-@pytest.mark.parametrize("nranks", [2, 8])
-def test_syn_1m_cpp_plans(nranks):
-    """syn-1M (BASELINE configs[3] mesh) split by the bench's own C++ partition into 2 and 8 ranks."""
+@pytest.mark.parametrize("nranks,mode", [(2, 0), (8, 0), (4, 1)])
+def test_syn_1m_cpp_plans(nranks, mode):
+    """syn-1M (BASELINE configs[3] mesh) split by the bench's own C++ partition into 2, 4 and 8 ranks (serial
+    semantics; OMP semantics at 4)."""
     from shud_rhs import synth
     m = synth.synth_model(1_000_000)
     m.step = workload.random_step_inputs(m)
     ep, _ = partition.cpp_partition(m, nranks, partition.PART_AUTO)
     locs = [partition.CppPlan(m, ep, nranks, r).local_model() for r in range(nranks)]
-    _run_ranks(m, [workload.random_state(m)], locs, 0, ncalls=2)
+    _run_ranks(m, [workload.random_state(m)], locs, mode, ncalls=2)
 
 
 def test_syn_10m_8way():
