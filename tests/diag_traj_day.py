@@ -3,7 +3,7 @@ integrator) and the CPU oracle chain (oracle RHS + oracle CVODE restatement), 10
 SHUD()'s loop (shud.cpp:89-140) with ccw.cfg.para's tolerances.  Per step: the error-weighted difference
 max_i |y_dev - y_cpu| / (rtol |y_cpu| + atol), the max absolute difference per state block, the total
 water volume difference (surface + unsaturated + groundwater, area-weighted) and both solvers' counters.
-usage: python tools/traj_day.py [out.json]"""
+usage: python tests/diag_traj_day.py [out.json]"""
 import json
 import os
 import sys

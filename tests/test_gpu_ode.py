@@ -10,7 +10,7 @@
     OMP semantics (stateless RHS): the gap stays ~1e-9 of the error weight over 6 simulated hours.  Serial
     semantics: the reference's carried u_satn/qEleE_IC make every RHS call depend on the previous one — including
     the difference-quotient J*v probes — and that feedback amplifies the pow/cbrt ulp differences ~10x per
-    10-minute solver step on ccw (tools/ode_diag.py), so serial runs are compared over the first hour only.
+    10-minute solver step on ccw (tests/diag_ode.py), so serial runs are compared over the first hour only.
     (The model itself is that sensitive: a 1-ulp perturbation of every initial state moves the CPU restatement's
     own ccw trajectory by 3e-2 of the error weight within 10 minutes, in either mode — branchy RHS.)
 (3) A physics error inside the integration surfaces as CV_RHSFUNC_FAIL and the reference exit code.

@@ -1,4 +1,4 @@
-"""Long-horizon trajectory agreement (tests/test_gpu_ode.py::test_ccw_one_day_trajectory, tools/traj_day.py):
+"""Long-horizon trajectory agreement (tests/test_gpu_ode.py::test_ccw_one_day_trajectory, tests/diag_traj_day.py):
 one simulated day of ccw through the device chain (RHS handle + device integrator) and the CPU oracle chain
 (oracle RHS + oracle CVODE restatement), 10-minute solver steps as SHUD()'s loop (shud.cpp:89-140) with
 ccw.cfg.para's tolerances (RELTOL = ABSTOL = 1e-4, INIT_SOLVER_STEP 1, MAX_SOLVER_STEP 10).  Per step: the
