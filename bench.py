@@ -33,6 +33,25 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def shared_partition(gm, world, rank, dist=None, device="cpu"):
+    """The N > 1 element partition: rank 0 runs the C++ partitioner (PART_AUTO, seed 12345; deterministic, so
+    any rank would get the same parts) and broadcasts the element -> part map and its stats over `dist`."""
+    import torch
+    from shud_rhs import partition
+    if rank == 0:
+        ele_part, pst = partition.cpp_partition(gm, world, partition.PART_AUTO, seed=12345)
+    else:
+        ele_part, pst = np.zeros(gm.num_ele, np.int32), None
+    if world > 1 and dist is not None:
+        t = torch.from_numpy(ele_part).to(device)
+        dist.broadcast(t, src=0)
+        ele_part = t.cpu().numpy()
+        box = [pst]
+        dist.broadcast_object_list(box, src=0)
+        pst = box[0]
+    return ele_part, pst
+
+
 def main():
     # stdout carries exactly one JSON line: libraries that print banners on it (RCCL prints its version block
     # at communicator init) write to stderr instead until the line is printed
@@ -90,17 +109,7 @@ def main():
         # halo wins; rank 0 partitions (deterministic: any rank would get the same parts) and broadcasts the
         # element -> part map, then every rank builds only its own plan
         tp = time.time()
-        if rank == 0:
-            ele_part, pst = partition.cpp_partition(gm, world, partition.PART_AUTO, seed=12345)
-        else:
-            ele_part, pst = np.zeros(gm.num_ele, np.int32), None
-        if world > 1:
-            ep_t = torch.from_numpy(ele_part).to(f"cuda:{local}")
-            dist.broadcast(ep_t, src=0)
-            ele_part = ep_t.cpu().numpy()
-            box = [pst]
-            dist.broadcast_object_list(box, src=0)
-            pst = box[0]
+        ele_part, pst = shared_partition(gm, world, rank, dist if world > 1 else None, f"cuda:{local}")
         cut_e, cut_s = pst["edge_cut"], pst["segment_cut"]
         plan = partition.CppPlan(gm, ele_part, world, rank)
         lm, part = plan.local_model()

@@ -158,8 +158,18 @@ def _gloo_worker(rank, world, port, outdir):
     import oracle
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, os.path.dirname(here))
+    import bench
     m, y = cases.variant(5000, seed=44)
-    ep, _ = partition.cpp_partition(m, world, partition.PART_MULTILEVEL)      # every rank: the same partition
+    # bench.py's N > 1 partition: rank 0 partitions, the map and stats are broadcast (here over gloo)
+    ep, pst = bench.shared_partition(m, world, rank, dist, "cpu")
+    ref, rst = partition.cpp_partition(m, world, partition.PART_AUTO, seed=12345)
+    same = {k: v for k, v in pst.items() if k != "seconds"} == {k: v for k, v in rst.items() if k != "seconds"}
+    if not (np.array_equal(ep, ref) and same):
+        with open(os.path.join(outdir, f"rank{rank}.txt"), "w") as f:
+            f.write("fail: broadcast partition differs")
+        dist.destroy_process_group()
+        return
     lm, part = partition.CppPlan(m, ep, world, rank).local_model()
     lo, to_o, from_o = _global_reach_order(lm, part)
     o = oracle.OracleRhs(lo, 0)
@@ -209,8 +219,9 @@ def _gloo_worker(rank, world, port, outdir):
 
 @pytest.mark.parametrize("world", [2, 4])
 def test_gloo_world_size(tmp_path, world):
-    """world_size 2 and 4 over gloo (127.0.0.1): each rank builds the C++ multilevel partition and its own
-    C++ plan, trades halos point to point, evaluates its local mesh with the oracle: owned DY bit-identical."""
+    """world_size 2 and 4 over gloo (127.0.0.1): rank 0 builds the C++ partition and broadcasts it (bench.py's
+    shared_partition), each rank builds its own C++ plan, trades halos point to point, evaluates its local mesh
+    with the oracle: owned DY bit-identical."""
     import torch.multiprocessing as mp
     port = _free_port()
     mp.start_processes(_gloo_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True,
