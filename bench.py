@@ -165,10 +165,15 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t_start
     ms_ele_loop, ms_riv_loop, ms_eval_loop, n_timed = h.timing_read()
+    kmax = None
     if world > 1:
         tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
+        # the slowest rank's in-loop kernel times (each rank's HIP events on its own compute stream)
+        kt = torch.tensor([ms_ele_loop, ms_riv_loop, ms_eval_loop], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(kt, op=dist.ReduceOp.MAX)
+        kmax = {"shud_ele_kernel": float(kt[0]), "shud_riv_kernel": float(kt[1]), "eval": float(kt[2])}
     err = h.get_error()
     if err["exit_code"]:
         log(f"[bench] WARNING physics error flags {err}")
@@ -226,6 +231,7 @@ def main():
             "kernel_ms": {k: v for k, v in per.items()},
             "kernel_ms_source": (f"HIP events around the kernels of {n_timed} of the {args.steps} timed evals "
                                  f"(1 in {t_stride}; handle stream)"),
+            **({"kernel_ms_max_over_ranks": kmax} if kmax else {}),
             "rhs_frac": (ele_bytes + riv_bytes) / (ms_eval * 1e-3) / HBM_PEAK,
             "riv_algorithmic_bytes_per_launch": riv_bytes,
             "riv_frac": riv_bytes / (ms_riv * 1e-3) / HBM_PEAK if ms_riv > 0 else None,
