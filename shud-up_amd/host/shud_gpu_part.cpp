@@ -16,6 +16,7 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <ctime>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -106,13 +107,34 @@ std::vector<double> test_state(const double *y0, int64_t ny, int ne, int k) {
     return y;
 }
 
-std::string read_file(const std::string &f) {
+// the RCCL id file of one job: "<token>\n" + 128 id bytes.  The token names the job (torchrun's run id and the
+// rendezvous address), so a file left by an earlier job in the same outdir is never taken for this one's
+std::string job_token() {
+    const char *run = getenv("TORCHELASTIC_RUN_ID"), *ma = getenv("MASTER_ADDR"), *mp = getenv("MASTER_PORT");
+    return std::string(run ? run : "-") + ":" + (ma ? ma : "-") + ":" + (mp ? mp : "-");
+}
+
+// the 128 id bytes of `f` if it carries `token` and was written after `not_before` (seconds since the epoch)
+std::string read_id_file(const std::string &f, const std::string &token, time_t not_before) {
+    struct stat st;
+    if (stat(f.c_str(), &st) != 0 || st.st_mtime < not_before) return "";
     FILE *fp = fopen(f.c_str(), "rb");
     if (!fp) return "";
-    std::string s(128, '\0');
-    const size_t n = fread(&s[0], 1, 128, fp);
+    std::string s(token.size() + 1 + 128, '\0');
+    const size_t n = fread(&s[0], 1, s.size(), fp);
     fclose(fp);
-    return n == 128 ? s : "";
+    if (n != s.size() || s.compare(0, token.size(), token) != 0 || s[token.size()] != '\n') return "";
+    return s.substr(token.size() + 1);
+}
+
+int mkdirs(const std::string &d) {
+    std::string cur;
+    for (size_t i = 0; i <= d.size(); i++) {
+        if ((i == d.size() || d[i] == '/') && !cur.empty()) mkdir(cur.c_str(), 0755);
+        if (i < d.size()) cur += d[i];
+    }
+    struct stat st;
+    return stat(d.c_str(), &st) == 0 ? 0 : -1;
 }
 
 }  // namespace
@@ -174,7 +196,9 @@ int shud_gpu_rhs_partition(shud_project_t p, int nparts_check, bool bench, int n
             shud_plan_gather_ele(q.plan, y_snow, lsn.data());
             const ShudEtMeshSoA le = local_et(q, etm);
             if (prepare_handle(q.h, le, etp, lis.data(), lsn.data(), q.ne, &f)) return 1;
-            const size_t no = 3 * (size_t)q.n_own + q.n_own_riv;
+            ShudPlanInfo I;
+            shud_plan_info(q.plan, &I);
+            const size_t no = 3 * (size_t)q.n_own + q.n_own_riv + I.n_own_lake;   // [sf|us|gw|riv|lake]
             q.y_own.resize(no);
             q.dy_own.resize(no);
             q.ref_own.resize(no);
@@ -259,20 +283,27 @@ int shud_gpu_rhs_partition(shud_project_t p, int nparts_check, bool bench, int n
         q.n_own = NE;
         q.n_own_riv = mesh.num_riv;
     } else {
-        mkdir(outdir.c_str(), 0755);
+        if (mkdirs(outdir)) { fprintf(stderr, "cannot create %s\n", outdir.c_str()); return 1; }
         const std::string idf = outdir + "/.shud_nccl_id";
+        const std::string token = job_token();
         if (rank == 0) {
+            unlink(idf.c_str());                              // never leave an earlier job's id in place
             char id[128];
             if (shud_rhs_nccl_unique_id(id)) return fail("nccl id");
             const std::string tmp = idf + ".tmp";
             FILE *fp = fopen(tmp.c_str(), "wb");
-            if (!fp || fwrite(id, 1, 128, fp) != 128) { fprintf(stderr, "cannot write %s\n", tmp.c_str()); return 1; }
+            if (!fp || fwrite(token.data(), 1, token.size(), fp) != token.size() || fputc('\n', fp) == EOF ||
+                fwrite(id, 1, 128, fp) != 128) {
+                fprintf(stderr, "cannot write %s\n", tmp.c_str());
+                return 1;
+            }
             fclose(fp);
             rename(tmp.c_str(), idf.c_str());
             nccl_id.assign(id, 128);
         } else {
+            const time_t not_before = time(nullptr) - 60;     // a file older than this job's start is stale
             for (int w = 0; w < 1200 && nccl_id.empty(); w++) {   // up to 120 s
-                nccl_id = read_file(idf);
+                nccl_id = read_id_file(idf, token, not_before);
                 if (nccl_id.empty()) std::this_thread::sleep_for(std::chrono::milliseconds(100));
             }
             if (nccl_id.empty()) { fprintf(stderr, "rank %d: no RCCL id in %s\n", rank, idf.c_str()); return 1; }
@@ -291,7 +322,12 @@ int shud_gpu_rhs_partition(shud_project_t p, int nparts_check, bool bench, int n
         const ShudEtMeshSoA le = local_et(q, etm);
         if (prepare_handle(h, le, etp, lis.data(), lsn.data(), q.ne, &f)) return 1;
     }
-    const size_t no = 3 * (size_t)q.n_own + q.n_own_riv;
+    size_t no = (size_t)ny;                                  // K = 1: the whole y, lakes included
+    if (K > 1) {
+        ShudPlanInfo I;
+        shud_plan_info(q.plan, &I);
+        no = 3 * (size_t)q.n_own + q.n_own_riv + I.n_own_lake;   // owned [sf|us|gw|riv|lake]
+    }
     const std::vector<double> y = test_state(y0, ny, NE, 0);
     std::vector<double> yo(no);
     if (K == 1) yo = y;

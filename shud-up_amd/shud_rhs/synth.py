@@ -223,10 +223,12 @@ def synth_raw(n_target, seed=12345, h=100.0, stem_every=12, reach_quads=3):
 
 
 def write_project(outdir, prj, n_target, days=2.0, seed=12345, max_step=10.0, et_step=60.0, dt_out=60,
-                  forcing_dt_min=60.0, extra_para=None, bc=False, cfg_output=False):
+                  forcing_dt_min=60.0, extra_para=None, bc=False, cfg_output=False, lake=False):
     """Write input files <outdir>/<prj>.* for the synthetic mesh; returns the in-memory ShudModel.
     bc: a few elements / reaches get boundary conditions (iBC = +-1, +-2; BC = +-1) with hourly .tsd.ebc1/.ebc2/
-    .rbc1/.rbc2 tables.  cfg_output: a .cfg.output switching some element / reach columns off."""
+    .rbc1/.rbc2 tables.  cfg_output: a .cfg.output switching some element / reach columns off.
+    lake: one lake (iLake = 1, MD_readin.cpp:262-263) over a 10 x 10-quad patch of the mesh, with a three-row
+    <prj>.lake.bathy (MD_Lake.cpp:147-168) and its stage as the cfg.ic's third table."""
     os.makedirs(outdir, exist_ok=True)
     m, raw = synth_raw(n_target, seed=seed)
     NE, NR, NS = m.num_ele, m.num_riv, m.num_seg
@@ -241,6 +243,12 @@ def write_project(outdir, prj, n_target, days=2.0, seed=12345, max_step=10.0, et
         ibc[pick_e] = [1, 2, 1, 2, -1, -2, -1, -2]
         pick_r = rng_bc.choice(NR, 4, replace=False)
         rbc[pick_r] = [1, -1, 1, -1]
+    ilake = np.zeros(NE, dtype=np.int64)
+    if lake:
+        nqx, nqy = grid_dims(n_target)
+        qi0, qj0 = nqx // 3, nqy // 3
+        qs = [(qj0 + b) * nqx + qi0 + a for b in range(10) for a in range(10)]
+        ilake[np.array([2 * q + t for q in qs for t in (0, 1)])] = 1
     p = lambda ext: os.path.join(outdir, f"{prj}.{ext}")
     nbr = m.nabr.reshape(3, NE)
     with open(p("sp.mesh"), "w") as f:
@@ -251,7 +259,11 @@ def write_project(outdir, prj, n_target, days=2.0, seed=12345, max_step=10.0, et
     pick = raw["pick"]
     with open(p("sp.att"), "w") as f:
         _write_table(f, ["INDEX", "SOIL", "GEOL", "LC", "FORC", "MF", "BC", "SS", "LAKE"],
-                     ([i + 1, pick[i, 0], pick[i, 1], pick[i, 2], 1, 1, ibc[i], 0, 0] for i in range(NE)))
+                     ([i + 1, pick[i, 0], pick[i, 1], pick[i, 2], 1, 1, ibc[i], 0, ilake[i]] for i in range(NE)))
+    if lake:
+        zl = float(np.min(m.ele["z_surf"][ilake > 0])) - 3.0
+        with open(p("lake.bathy"), "w") as f:
+            _write_table(f, ["Index", "Y", "Area"], [[1, zl, 2.0e4], [2, zl + 5.0, 1.5e5], [3, zl + 20.0, 4.0e5]])
     for ext, tab in (("para.soil", raw["soil"]), ("para.geol", raw["geol"]), ("para.lc", raw["lc"])):
         with open(p(ext), "w") as f:
             _write_table(f, [f"C{j}" for j in range(tab.shape[1])], ([int(r[0])] + [float(v) for v in r[1:]] for r in tab))
@@ -291,6 +303,8 @@ def write_project(outdir, prj, n_target, days=2.0, seed=12345, max_step=10.0, et
                      ([i + 1, 0.0, 0.0, float(rng.uniform(0, 0.01)), float(0.2 * aq[i]), float(0.6 * aq[i])]
                       for i in range(NE)))
         _write_table(f, ["Index", "Stage"], ([r + 1, float(rng.uniform(0.1, 1.0))] for r in range(NR)))
+        if lake:
+            _write_table(f, ["Index", "Stage"], [[1, 3.5]])
     # forcing: one station (ccw's coordinates), hourly prcp/temp/rh/wind/radiation, 20000101
     nrow = int(np.ceil(days * 1440.0 / forcing_dt_min)) + 2
     tday = np.arange(nrow) * forcing_dt_min / 1440.0

@@ -146,14 +146,16 @@ def test_device_loop_vs_oracle_chain_first_hour(tmp_path):
     h.close()
 
 
-@pytest.mark.parametrize("parts", [2, 4, 8])
-def test_shud_gpu_rhs_partition_check(tmp_path, parts):
+@pytest.mark.parametrize("parts,lake", [(2, False), (4, False), (8, False), (2, True), (3, True)])
+def test_shud_gpu_rhs_partition_check(tmp_path, parts, lake):
     """shud_gpu --rhs-check K: the C++ host partitions a synthetic project (C++ partitioner + planner), drives K
     partitioned RHS handles on one GPU with the halo moved by D2D copies and the ET prelude run on every local
-    mesh, and compares every owned DY with the unpartitioned handle's: zero mismatched entries (bit-identical)."""
+    mesh, and compares every owned DY with the unpartitioned handle's: zero mismatched entries (bit-identical).
+    lake: a project with one lake (200 lake elements); the owned state of the lake's rank carries the lake stage
+    after its reaches ([sf|us|gw|riv|lake]) and the lake's DY is compared too."""
     import json
     src = tmp_path / "in"
-    synth.write_project(str(src), "syn", 30000, days=1.0, max_step=10.0, et_step=60.0, dt_out=60)
+    synth.write_project(str(src), "syn", 30000, days=1.0, max_step=10.0, et_step=60.0, dt_out=60, lake=lake)
     r = subprocess.run([SHUD_GPU, "--rhs-check", str(parts), "--evals", "6", "-C", str(src), str(src), "syn"],
                        capture_output=True, text=True, timeout=240)
     line = [ln for ln in r.stdout.splitlines() if ln.startswith('{"shud_gpu_rhs_check"')]
@@ -163,11 +165,13 @@ def test_shud_gpu_rhs_partition_check(tmp_path, parts):
     assert res["max_ghost_ele"] > 0 and res["imbalance"] < 1.05
 
 
-def test_shud_gpu_rhs_bench_single_rank(tmp_path):
-    """shud_gpu --rhs-bench with WORLD_SIZE = 1 (the N > 1 mode runs one process per GPU over RCCL)."""
+@pytest.mark.parametrize("lake", [False, True])
+def test_shud_gpu_rhs_bench_single_rank(tmp_path, lake):
+    """shud_gpu --rhs-bench with WORLD_SIZE = 1 (the N > 1 mode runs one process per GPU over RCCL); with a lake
+    the device state holds the lake stage after the reaches."""
     import json
     src = tmp_path / "in"
-    synth.write_project(str(src), "syn", 30000, days=1.0, max_step=10.0, et_step=60.0, dt_out=60)
+    synth.write_project(str(src), "syn", 30000, days=1.0, max_step=10.0, et_step=60.0, dt_out=60, lake=lake)
     env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
     r = subprocess.run([SHUD_GPU, "--rhs-bench", "--evals", "20", "-o", str(tmp_path / "o"), "-C", str(src),
                         str(src), "syn"], capture_output=True, text=True, timeout=240, env=env)

@@ -67,8 +67,11 @@ def test_run_to_run_determinism(n, seed, mode):
         assert np.array_equal(d0[k], d1[k], equal_nan=True), k
 
 
-@SETTINGS
-@given(blocks=st.one_of(st.integers(0, 300), st.integers(2040, 2600)), tail=st.integers(1, 255),
+# the CPU restatement integrates sequentially: sizes just past the 2048-block reduction grid exercise the
+# grid-stride tail without spending minutes in the oracle (12 examples up to 2600 blocks took 133 s)
+@settings(max_examples=8, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+@given(blocks=st.one_of(st.integers(0, 300), st.integers(2044, 2100)), tail=st.integers(1, 255),
        rtol_e=st.integers(4, 8), atol_e=st.integers(8, 12), h0_e=st.integers(2, 6))
 def test_integrator_random_sizes_bit_identical(blocks, tail, rtol_e, atol_e, h0_e):
     """decayn with n = 256*blocks + tail: the reduction grid (min(ceil(n/256), 2048) blocks, grid-stride:
