@@ -70,6 +70,13 @@ enum ClassField {
 // record stride of the class table (8-B words), odd: lanes reading one field of different classes from the
 // LDS copy land on different banks (an even stride of 32 put every class on one bank)
 constexpr int CF_STRIDE = CF_COUNT | 1;
+// divisors that cdiv (shud_physics.h) may take with a host reciprocal: 0, +-inf, NaN, or |b| in [kCdivBmin,
+// kCdivBmax] (the handle checks every such divisor at create and otherwise keeps the plain-division layout)
+constexpr double kCdivBmin = 0x1p-20, kCdivBmax = 0x1p20;
+inline bool cdiv_divisor_ok(double b) {
+    const double a = b < 0 ? -b : b;
+    return b == 0. || !(a < 1e308) || (a >= kCdivBmin && a <= kCdivBmax);    // !(a < 1e308): inf or NaN
+}
 // most classes one workgroup stages in LDS (128 x 33 x 8 B = 33 KiB)
 #ifndef SHUD_LDS_CLS_MAX
 #define SHUD_LDS_CLS_MAX 128
@@ -102,9 +109,21 @@ struct DevPacked {
     // depth, (down, BC)}: everything a reach's own, its downstream's and its upstream reaches' QrivDown read,
     // so a neighbour reach costs one cache line instead of one line per field pair
     const double2 *rv;      // [4 * NR]
-    const int4 *rv_i;       // {down, BC, first reach-sorted segment, #segments}
-    const int4 *rv_u;       // {up0, up1, up2, #up} (ascending global order); #up = -1: use up_off/up_idx
+    const int4 *rv_i;       // owned reaches: {first reach-sorted segment, #segments, first upstream record, #up}
+    // owned reaches: the downstream term's statics, 32 B {smean = (slope + slope_down) * 0.5, depth_down |
+    // RN(1/Dist2DownStream), (down or self, BC of down)} — the downstream reach costs its 8-B stage only
+    const double2 *rv_dn;   // [2 * n_own_riv]
+    // one 64-B record per (owned reach, upstream reach), CSR in ascending (global) upstream order (MD_f.cpp:
+    // 236-240): the upstream reach's QrivDown statics {BottomWidth, bankslope | depth, Dist2DownStream |
+    // avgRough, smean = (slope_u + slope) * 0.5 | (u, BC_u), RN(1/Dist2DownStream_u)} — contiguous per reach
+    // instead of one scattered 64-B line per upstream reach
+    const double2 *upr;     // [4 * #upstream edges]
+    // correctly rounded reciprocals of static geometric divisors, uploaded only for a kernel built with the
+    // matching SHUD_RCP bit (shud_ele_rcp_mask()): 1 area, 2 Dist2Nabor [3][NE], 4 segment reach BedThick
+    const double *r_area, *r_d2n, *sg_rbt;
 };
+// SHUD_RCP mask the packed element kernel was compiled with (shud_ele_packed.hip)
+int shud_ele_rcp_mask();
 
 struct DevDiag {                     // optional diagnostic outputs (ShudFluxOut), local numbering
     double *qele_surf, *qele_sub, *qele_surf_tot, *qele_sub_tot, *q_infil, *q_exfil, *q_recharge;
@@ -152,7 +171,7 @@ void launch_element_kernel(const DevMesh &m, const YView &Y, double *dy, int n_c
                            int mode, bool open, bool diag, const DevDiag &dg, hipStream_t s, int variant = 0);
 void launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1,
                                   int cur, int mode, bool open, bool diag, bool fu_unit, const DevDiag &dg,
-                                  hipStream_t s, const DevLake *lake = nullptr);
+                                  hipStream_t s, const DevLake *lake = nullptr, bool interior = false);
 void launch_river_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int mode,
                                 bool diag, const DevDiag &dg, hipStream_t s);
 void launch_lake_kernel(const DevMesh &m, const DevPacked &p, const DevLake &L, const YView &Y, double *dy,

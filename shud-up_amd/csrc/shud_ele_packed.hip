@@ -42,7 +42,22 @@ __device__ __forceinline__ void stnt2(double2 *p, double a, double b) {
     v.y = b;
     __builtin_nontemporal_store(v, (v2d *)p);
 }
+// element / segment streams are addressed as a wave-uniform base + a 32-bit byte offset, which the compiler
+// emits as global_load/store v, vOff, s[base] (saddr form): one 32-bit shift per record size shared by every
+// stream of that size, instead of a sign extension and a 64-bit address add per stream.  The handle keeps
+// every such array below 4 GiB (build_packed: 48 B x NE and 16 B x NS).
+template <class T>
+__device__ __forceinline__ const T *at(const T *b, uint32_t off) { return (const T *)((const char *)b + off); }
+template <class T>
+__device__ __forceinline__ T *atw(T *b, uint32_t off) { return (T *)((char *)b + off); }
 
+// SHUD_RCP (A/B of host reciprocals for static geometric divisors through cdiv; bit-identical either way):
+// bit 0 area (2 divisions per element + the eqbc term), bit 1 Dist2Nabor (2 per edge), bit 2 BedThick (1 per
+// segment).  Each costs 8 B of HBM per divisor instance and saves ~5 VALU per division.
+#ifndef SHUD_RCP
+#define SHUD_RCP 0
+#endif
+int shud_ele_rcp_mask() { return SHUD_RCP; }
 #ifndef SHUD_AREA_EARLY
 #define SHUD_AREA_EARLY 1
 #endif
@@ -92,20 +107,22 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     if (i >= n_compute) return;
     const int NEl = m.num_ele;
     const int nown = Y.n_own;
-
     // ---------------- own records first; saturation (its two pow calls are the register peak) is computed
     // while little else is live ----------------
-    const int4 mt = p.meta[i];
-    const double2 zz = p.zz[i];
-    const double ysf_raw = Y.sf_<GH>(i), yus_raw = Y.us_<GH>(i), ygw_raw = Y.gw_<GH>(i);
+    const uint32_t o16 = (uint32_t)i << 4, o8 = (uint32_t)i << 3;
+    const int4 mt = *at(p.meta, o16);
+    const double2 zz = *at(p.zz, o16);
+    const double ysf_raw = GH ? Y.sf(i) : *at(Y.y, o8);
+    const double yus_raw = GH ? Y.us(i) : *at(Y.y + nown, o8);
+    const double ygw_raw = GH ? Y.gw(i) : *at(Y.y + 2 * (size_t)nown, o8);
     const int cf = mt.w;
     const int cid = cf_class(cf), ibc = cf_ibc(cf);
     const bool is_lake = LAKE && cf < 0;
-    const double2 snp = ldnt2(&p.s_np[i]), stl = ldnt2(&p.s_tl[i]);
-    const double etp = ldnt(&m.etp[i]);
+    const double2 snp = ldnt2(at(p.s_np, o16)), stl = ldnt2(at(p.s_tl, o16));
+    const double etp = ldnt(at(m.etp, o8));
     double2 fu;
-    if (FU1) { fu.x = 1.0; fu.y = 1.0; } else fu = ldnt2(&p.s_fu[i]);
-    const double2 csv = ldnt2(&p.cs[cur][i]);
+    if (FU1) { fu.x = 1.0; fu.y = 1.0; } else fu = ldnt2(at(p.s_fu, o16));
+    const double2 csv = ldnt2(at(p.cs[cur], o16));
 #define CL(f) (LCT ? lct[cid * CF_LDS_STRIDE + CF_##f] : p.ctab[cid * CF_STRIDE + CF_##f])
 #define CDIV(a, F) CDIV_(a, CL(F), CL(r_##F))
 
@@ -134,7 +151,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         }
     }
 
-    const int sfirst = p.seg_first[i];
+    const int sfirst = *at(p.seg_first, (uint32_t)i << 2);
     const int iss = cf_iss(cf), nseg = cf_nseg(cf);
     const double infD = CL(infD), ThR = CL(ThetaR);
     const double infK = CL(infKsatV);
@@ -172,7 +189,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         if (DIAG) { dg.q_es[i] = Es; dg.q_eu[i] = Eu; dg.q_eg[i] = Eg; dg.q_tu[i] = Tu; dg.q_tg[i] = Tg;
                     dg.q_eta[i] = eta; dg.i_beta[i] = ibeta; }
     }
-    stnt2(&p.cs[cur ^ 1][i], satn, eic);
+    stnt2(atw(p.cs[cur ^ 1], o16), satn, eic);
 
     // ---- Flux_Infiltration (Element.cpp:271-303) and Flux_Recharge (:304-335); zero on lake elements ----
     double qi = 0., qex = 0., qr = 0.;
@@ -210,7 +227,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     // dgw = (recharge - exfil) - Qsub/area - Eg - Tg.  Ends the ET/vertical live ranges early.
     const double dsf_head = snp.x - q_infil + q_exfil;
     const double dgw_head = q_rech - q_exfil;
-    if (i < nown) __builtin_nontemporal_store(is_lake ? 0. : CDIV(q_infil - q_rech - Eu - Tu, Sy), &dy[nown + i]);
+    if (i < nown) __builtin_nontemporal_store(is_lake ? 0. : CDIV(q_infil - q_rech - Eu - Tu, Sy), atw(dy + nown, o8));
 
     // ---- own river segments (fun_Seg_surface / fun_Seg_sub) and Qe2r (PassValue) ----
     const double dep = CL(depression), rgh = CL(rough);
@@ -219,16 +236,22 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         const double isf_seg = rmax(0., usf - q_infil + q_exfil);
         for (int k = sfirst, k1 = k + nseg; k < k1; k++) {
             // one 48-B element-sorted record per segment: its own fields plus its reach's statics
-            const double2 lc = p.sg_lc[k], dk = p.sg_dk[k];
-            const int2 rb = p.sg_rb[k];
-            const double bt = p.sg_bt[k];
-            double yr = Y.riv_<GH>(rb.x);                 // uriv_of (shud_physics.h), BC from the record
+            const uint32_t k16 = (uint32_t)k << 4, k8 = (uint32_t)k << 3;
+            const double2 lc = *at(p.sg_lc, k16), dk = *at(p.sg_dk, k16);
+            const int2 rb = *at(p.sg_rb, k8);
+            const double bt = *at(p.sg_bt, k8);
+            double yr = GH ? Y.riv(rb.x) : *at(Y.y + 3 * (size_t)nown, (uint32_t)rb.x << 3);   // uriv_of, BC below
             if (MODE == 1) yr = (yr >= 0.) ? yr : 0.;
             if (rb.y > 0) yr = m.rybc[rb.y];
             const double rdep = dk.x, L = lc.x;
             const double qs = weir_jtoi(zs, isf_seg, zs - rdep, yr, zs + 0.0, lc.y, L, dep);
+#if SHUD_RCP & 4
+            const double qg = r2e_gw<true>(yr, zs - rdep, ugw, zb, ekh, dk.y, L, bt, *at(p.sg_rbt, k8)) * fu_sub;
+#else
             const double qg = r2e_gw(yr, zs - rdep, ugw, zb, ekh, dk.y, L, bt) * fu_sub;
-            p.qseg2[p.seg_rpos ? p.seg_rpos[k] : k] = make_double2(qs, qg);   // element-sorted by default
+#endif
+            if (p.seg_rpos) p.qseg2[p.seg_rpos[k]] = make_double2(qs, qg);
+            else *atw(p.qseg2, k16) = make_double2(qs, qg);                  // element-sorted (default)
             qe2r_surf += -qs;
             qe2r_sub += -qg;
         }
@@ -247,17 +270,25 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     bool nan_q = false;
     const double isf = usf < 0. ? 0. : usf;
 #if SHUD_AREA_EARLY
-    const double area = ldnt(&p.area[i]);              // in flight across the edge loop
+    const double area = ldnt(at(p.area, o8));          // in flight across the edge loop
 #endif
 #pragma unroll 1
     for (int j = 0; j < (is_lake ? 0 : 3); j++) {     // lake elements: fun_Ele_lakeHorizon, all zero
         const int nb = j == 0 ? mt.x : j == 1 ? mt.y : mt.z;
-        const double2 g = ldnt2(&p.ged[(size_t)j * NEl + i]);
+        const double2 g = ldnt2(at(p.ged + (size_t)j * NEl, o16));
         const int nc = nb >= 0 ? nb : i;                  // boundary edge: harmless in-bounds loads
-        const double2 nzz = p.zz[nc];
-        const int ncf = p.meta[nc].w;
-        const double nsf_raw = Y.sf_<GH>(nc), ngw_raw = Y.gw_<GH>(nc);
+        const uint32_t n16 = (uint32_t)nc << 4, n8 = (uint32_t)nc << 3;
+        const double2 nzz = *at(p.zz, n16);
+        const int ncf = *at((const int *)p.meta + 3, n16);
+        const double nsf_raw = GH ? Y.sf(nc) : *at(Y.y, n8);
+        const double ngw_raw = GH ? Y.gw(nc) : *at(Y.y + 2 * (size_t)nown, n8);
         const double B = g.x, d2n = g.y;
+#if SHUD_RCP & 2
+        const double rd2n = ldnt(at(p.r_d2n + (size_t)j * NEl, o8));
+#define D2N_DIV(a) CDIV_(a, d2n, rd2n)
+#else
+#define D2N_DIV(a) SDIV(a, d2n)
+#endif
         double qsf = 0., qsb = 0.;
         const int cn = cf_class(ncf);
 #define CN(f) (LCT ? lct[cn * CF_LDS_STRIDE + CF_##f] : p.ctab[cn * CF_STRIDE + CF_##f])
@@ -273,7 +304,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
             else if (dhg < 0. && yl <= 0.02) q = 0.;
             else {
                 const double ymg = (rmax(ugw, 0.) + rmax(yl, 0.)) * .5;
-                const double grad = SDIV(dhg, d2n);
+                const double grad = D2N_DIV(dhg);
                 const double kmean = 0.5 * (ekh + CN(KsatH));            // the lake element's u_effKH = KsatH
                 q = kmean * grad * ymg * B;
             }
@@ -289,7 +320,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
             double ym = ((isf + zs) > (nsf + zsn)) ? ((isf > dep) ? isf : 0.) : ((nsf > dep) ? nsf : 0.);
             ym = rmin(ym, K_MAXYSURF);
             if (ym > 0.) {
-                const double s = SDIV(dh, d2n);
+                const double s = D2N_DIV(dh);
                 if (s > 0 && isf <= 0) qsf = 0.;
                 else if (s < 0 && nsf <= 0) qsf = 0.;
                 else qsf = manning(ym * B, 0.5 * (rgh + CN(rough)), ym, s);   // avgRough, Element.cpp:253
@@ -303,7 +334,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
             else {
                 const double ekn = eff_kh(ugn, zsn - zbn, CN(macD), CN(macKsatH), CN(vAreaF), CN(KsatH));
                 const double ymg = (rmax(ugw, 0.) + rmax(ugn, 0.)) * .5;
-                const double grad = SDIV(dhg, d2n);
+                const double grad = D2N_DIV(dhg);
                 const double kmean = 0.5 * (ekh + ekn);
                 q = kmean * grad * ymg * B;
             }
@@ -324,6 +355,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
             qsb = q * fu_sub;
         }
 #undef CN
+#undef D2N_DIV
         if (MODE == 0) nan_q |= nan_or_inf(qsf) || nan_or_inf(qsb);
         sumsurf += qsf;
         sumsub += qsb;
@@ -335,19 +367,26 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
 
     // ---- f_applyDY element part (MD_f.cpp:88-150 / MD_f_omp.cpp:26-46) ----
 #if !SHUD_AREA_EARLY
-    const double area = ldnt(&p.area[i]);
+    const double area = ldnt(at(p.area, o8));
 #endif
-    double dsf = dsf_head - SDIV(sumsurf, area) - Es;
-    double dgw = dgw_head - SDIV(sumsub, area) - Eg - Tg;
+#if SHUD_RCP & 1
+    const double rarea = ldnt(at(p.r_area, o8));
+#define AREA_DIV(a) CDIV_(a, area, rarea)
+#else
+#define AREA_DIV(a) SDIV(a, area)
+#endif
+    double dsf = dsf_head - AREA_DIV(sumsurf) - Es;
+    double dgw = dgw_head - AREA_DIV(sumsub) - Eg - Tg;
     if (ibc > 0) dgw = 0;
-    else if (ibc < 0) dgw += SDIV(m.eqbc[-ibc], area);
-    if (iss == 1) dsf += 0.0 / area;                          // QSS is never assigned: 0
-    else if (iss == 2) dgw += 0.0 / area;
+    else if (ibc < 0) dgw += AREA_DIV(m.eqbc[-ibc]);
+#undef AREA_DIV
+    if (iss == 1) dsf += zero_over(area);                     // QSS is never assigned: 0.0 / area
+    else if (iss == 2) dgw += zero_over(area);
     dgw = CDIV(dgw, Sy);
     if (is_lake) { dsf = 0.; dgw = 0.; }                      // MD_f.cpp:146-150
 #undef CL
-    __builtin_nontemporal_store(dsf, &dy[i]);
-    __builtin_nontemporal_store(dgw, &dy[2 * nown + i]);
+    __builtin_nontemporal_store(dsf, atw(dy, o8));
+    __builtin_nontemporal_store(dgw, atw(dy + 2 * (size_t)nown, o8));
     if (DIAG) { dg.qele_surf_tot[i] = sumsurf; dg.qele_sub_tot[i] = sumsub; }
 }
 
@@ -377,12 +416,14 @@ __device__ __forceinline__ double riv_stage_p(const DevMesh &m, const YView &Y, 
     *yg = yr;
     return bc > 0 ? m.rybc[bc] : yr;
 }
-// MD_RiverFlux.cpp:5-63: reach q with stage uq and geometry g; its downstream has stage ud, depth, slope
+// MD_RiverFlux.cpp:5-63: QrivDown of reach q with stage uq and geometry g.  Towards a downstream reach (down >= 0)
+// the slope term is ((uq - depth) - (ud - ddepth)) / Dist2DownStream + smean with the host's smean = (slope +
+// slope_down) * 0.5 (same operations, same order) and the division through cdiv with the host reciprocal
+// rd2d (bit-identical, shud_physics.h); outlets as before.
 __device__ __forceinline__ double riv_down_p(const RivP &q, double uq, const RivGeom &g, double ud, double ddepth,
-                                             double dslope) {
+                                             double smean, double rd2d) {
     if (q.down >= 0) {
-        const double smean = (q.slope + dslope) * 0.5;
-        const double s = ((uq - q.depth) - (ud - ddepth)) / q.d2d + smean;
+        const double s = CDIV_((uq - q.depth) - (ud - ddepth), q.d2d, rd2d) + smean;
         const double R = (g.csperem <= K_ZERO) ? 0. : (g.csarea / g.csperem);
         return manning(g.csarea, q.n, R, s);
     } else if (q.down >= -3) {
@@ -392,54 +433,49 @@ __device__ __forceinline__ double riv_down_p(const RivP &q, double uq, const Riv
     }
     return g.csarea * sqrt(K_GRAV * uq) * 60.;
 }
+// outlet form only (a reach flowing into a lake, the lake kernel's QLakeRivIn: down = -3 on the record)
+__device__ __forceinline__ double riv_down_outlet(const RivP &q, double uq, const RivGeom &g) {
+    return riv_down_p(q, uq, g, 0., 0., 0., 0.);
+}
 
-// ABL (timing-only ablations, SHUD_RIV_ABL; results are wrong when != 0): bit 0 skips the upstream
+// ABL (timing-only ablation builds, -DSHUD_RIV_ABL=k; results are wrong when != 0): bit 0 skips the upstream
 // reaches, bit 1 the segment gathers, bit 2 the downstream reach
+#ifndef SHUD_RIV_ABL
+#define SHUD_RIV_ABL 0
+#endif
 template <int MODE, bool DIAG, int ABL = 0>
 __global__ void __launch_bounds__(256)
 shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, DevDiag dg) {
-    // XCD-chunked workgroup order: a reach's up/downstream records sit a few blocks away in index space,
-    // so they are L2 hits on the same XCD instead of fabric round trips (speed only)
+    // XCD-chunked workgroup order: neighbouring reaches' segment fluxes and stages share an XCD's L2 (speed only)
     const int r = block_id<1>() * blockDim.x + threadIdx.x;
     if (r >= Y.n_own_riv) return;
     const RivP q = riv_load(p, r);
-    const int4 ii = p.rv_i[r];                                  // {down, BC, first segment, #segments}
-    const int4 up = p.rv_u[r];
+    const int4 ii = p.rv_i[r];                                  // {first segment, #segments, first up, #up}
+    const double2 dn0 = p.rv_dn[2 * (size_t)r], dn1 = p.rv_dn[2 * (size_t)r + 1];
     double yg;
     const double ur = riv_stage_p<MODE>(m, Y, r, q.bc, &yg);
     const RivGeom g = riv_geom_p(q, yg);
     double qdown = 0.;
     if (!(ABL & 4)) {
-        const int d = q.down >= 0 ? q.down : r;                 // clamped: unconditional loads
-        const double2 bd = p.rv[4 * (size_t)d + 1], dd = p.rv[4 * (size_t)d + 3];   // same line of d's record
-        const int bcd = rv_ib(dd.y).y;
+        const int2 db = rv_ib(dn1.y);                           // (down or self, BC of down): unconditional load
         double ydg;
-        const double ud = riv_stage_p<MODE>(m, Y, d, bcd, &ydg);
-        qdown = riv_down_p(q, ur, g, ud, dd.x, bd.y);
+        const double ud = riv_stage_p<MODE>(m, Y, db.x, db.y, &ydg);
+        qdown = riv_down_p(q, ur, g, ud, dn0.y, dn0.x, dn1.x);
     }
-    // junction: QrivUp[down] += -QrivDown[i], i ascending (MD_f.cpp:236-240)
+    // junction: QrivUp[down] += -QrivDown[i], i ascending (MD_f.cpp:236-240).  Each upstream reach's QrivDown
+    // (towards this reach) from its contiguous record and its 8-B stage
     double qup = 0.;
-    const int nup = (ABL & 1) ? 0 : up.w;
-    if (nup >= 0) {
-        const int uv[3] = {up.x, up.y, up.z};
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-            if (k < nup) {
-                const int u = uv[k];
-                const RivP qu = riv_load(p, u);
-                double yu;
-                const double uu = riv_stage_p<MODE>(m, Y, u, qu.bc, &yu);
-                qup += -riv_down_p(qu, uu, riv_geom_p(qu, yu), ur, q.depth, q.slope);
-            }
-        }
-    } else {
-        for (int k = m.up_off[r], k1 = m.up_off[r + 1]; k < k1; k++) {
-            const int u = m.up_idx[k];
-            const RivP qu = riv_load(p, u);
-            double yu;
-            const double uu = riv_stage_p<MODE>(m, Y, u, qu.bc, &yu);
-            qup += -riv_down_p(qu, uu, riv_geom_p(qu, yu), ur, q.depth, q.slope);
-        }
+    const int nup = (ABL & 1) ? 0 : ii.w;
+    for (int k = ii.z, k1 = ii.z + nup; k < k1; k++) {
+        const double2 *u4 = p.upr + 4 * (size_t)k;
+        const double2 a = u4[0], b = u4[1], c = u4[2], d = u4[3];
+        const int2 ub = rv_ib(d.x);
+        double yu;
+        const double uu = riv_stage_p<MODE>(m, Y, ub.x, ub.y, &yu);
+        const RivGeom gu = riv_geom(a.x, a.y, 0., yu);
+        const double s = CDIV_((uu - b.x) - (ur - q.depth), b.y, d.y) + c.y;
+        const double R = (gu.csperem <= K_ZERO) ? 0. : (gu.csarea / gu.csperem);
+        qup += -manning(gu.csarea, c.x, R, s);
     }
     // segment sums, ascending reference segment order (MD_f.cpp:228-235), gathered from the element-sorted
     // fluxes (scattered 8-B writes from the element kernel cost more than these gathers).  Batches of 8:
@@ -447,13 +483,13 @@ shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     double qsurf = 0., qsub = 0.;
     if (ABL & 2) {
     } else if (p.seg_rpos) {                            // reach-sorted fluxes: this reach's segments are contiguous
-        for (int k = ii.z, k1 = ii.z + ii.w; k < k1; k++) {
+        for (int k = ii.x, k1 = ii.x + ii.y; k < k1; k++) {
             const double2 q2 = p.qseg2[k];
             qsurf += q2.x;
             qsub += q2.y;
         }
     } else
-    for (int k0 = ii.z, k1 = ii.z + ii.w; k0 < k1; k0 += 8) {
+    for (int k0 = ii.x, k1 = ii.x + ii.y; k0 < k1; k0 += 8) {
         int ps[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) ps[j] = m.rseg_pos[k0 + j < k1 ? k0 + j : k0];
@@ -482,18 +518,13 @@ void launch_river_kernel_packed(const DevMesh &m, const DevPacked &p, const YVie
                                 bool diag, const DevDiag &dg, hipStream_t s) {
     if (Y.n_own_riv <= 0) return;
     const dim3 grid(((Y.n_own_riv + 255) / 256 + 7) / 8 * 8), blk(256);
-    const char *abl_env = getenv("SHUD_RIV_ABL");
-    const int abl = abl_env ? atoi(abl_env) : 0;
-    if (abl && mode == 0 && !diag) {
-        switch (abl & 7) {
-        case 1: hipLaunchKernelGGL((shud_riv_kernel_packed<0, false, 1>), grid, blk, 0, s, m, p, Y, dy, dg); return;
-        case 2: hipLaunchKernelGGL((shud_riv_kernel_packed<0, false, 2>), grid, blk, 0, s, m, p, Y, dy, dg); return;
-        case 3: hipLaunchKernelGGL((shud_riv_kernel_packed<0, false, 3>), grid, blk, 0, s, m, p, Y, dy, dg); return;
-        case 4: hipLaunchKernelGGL((shud_riv_kernel_packed<0, false, 4>), grid, blk, 0, s, m, p, Y, dy, dg); return;
-        case 7: hipLaunchKernelGGL((shud_riv_kernel_packed<0, false, 7>), grid, blk, 0, s, m, p, Y, dy, dg); return;
-        default: break;
-        }
+#if SHUD_RIV_ABL
+    // timing-only ablation build (tools/riv_abl.sh: -DSHUD_RIV_ABL=k); never part of the production library
+    if (mode == 0 && !diag) {
+        hipLaunchKernelGGL((shud_riv_kernel_packed<0, false, SHUD_RIV_ABL>), grid, blk, 0, s, m, p, Y, dy, dg);
+        return;
     }
+#endif
     if (mode == 0) {
         if (diag) hipLaunchKernelGGL((shud_riv_kernel_packed<0, true>), grid, blk, 0, s, m, p, Y, dy, dg);
         else hipLaunchKernelGGL((shud_riv_kernel_packed<0, false>), grid, blk, 0, s, m, p, Y, dy, dg);
@@ -567,7 +598,7 @@ shud_lake_kernel(DevMesh m, DevPacked p, DevLake L, YView Y, double *__restrict_
         const RivP q = riv_load(p, r);
         double yg;
         const double ur = riv_stage_p<0>(m, Y, r, q.bc, &yg);
-        return riv_down_p(q, ur, riv_geom_p(q, yg), 0., 0., 0.);          // q.down = -3: outlet formula
+        return riv_down_outlet(q, ur, riv_geom_p(q, yg));                // q.down = -3: outlet formula
     }, buf);
     if (threadIdx.x == 0) {
         const double zmin = L.bathy_y[L.bathy_off[l]];
@@ -612,12 +643,14 @@ static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, doubl
 
 void launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1,
                                   int cur, int mode, bool open, bool diag, bool fu_unit, const DevDiag &dg,
-                                  hipStream_t s, const DevLake *lake) {
+                                  hipStream_t s, const DevLake *lake, bool interior) {
     if (i1 <= i0) return;
     DevLake lk{};
     if (lake) lk = *lake;
-    // lakes: serial semantics only (the handle rejects OMP + lakes), class table in LDS, with or without ghosts
-    const bool gh = Y.gele != nullptr || Y.griv != nullptr;      // partitioned handle: ghost entities
+    // lakes: serial semantics only (the handle rejects OMP + lakes), class table in LDS, with or without ghosts.
+    // A partitioned handle's interior elements (interior = true: every lateral neighbour and every segment's
+    // reach owned) read only owned state, so they take the ghost-free instantiation (direct y addressing).
+    const bool gh = !interior && (Y.gele != nullptr || Y.griv != nullptr);
 #define LP(MO, OP, DI, FU) do {                                                                            \
         if (lake && MO == 0) {                                                                            \
             if (gh) launch_p<MO, OP, DI, FU, true, true, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s);      \

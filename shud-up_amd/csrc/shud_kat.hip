@@ -132,3 +132,32 @@ extern "C" void shud_kat_ode_free(void *user) {
     (void)hipStreamDestroy(u->s);
     delete u;
 }
+
+// cdiv (shud_physics.h) on host-given (a, b) pairs with the host's correctly rounded rb = 1/b, as the handle
+// supplies it (tests/test_kat.py::test_cdiv_bit_identical compares against IEEE a / b)
+__global__ void kat_cdiv_kernel(const double *__restrict__ a, const double *__restrict__ b,
+                                const double *__restrict__ rb, int n, double *__restrict__ out) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n) out[t] = cdiv(a[t], b[t], rb[t]);
+}
+extern "C" int shud_kat_cdiv(const double *h_a, const double *h_b, int n, double *h_out) {
+    if (n <= 0) return -1;
+    std::vector<double> rb(n);
+    for (int k = 0; k < n; k++) rb[k] = 1. / h_b[k];
+    double *d = nullptr;
+    const size_t bytes = sizeof(double) * (size_t)n;
+    if (hipMalloc(&d, 4 * bytes) != hipSuccess) return -3;
+    int rc = 0;
+    if (hipMemcpy(d, h_a, bytes, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d + n, h_b, bytes, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d + 2 * (size_t)n, rb.data(), bytes, hipMemcpyHostToDevice) != hipSuccess)
+        rc = -3;
+    if (!rc) {
+        hipLaunchKernelGGL(kat_cdiv_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, d, d + n, d + 2 * (size_t)n, n,
+                           d + 3 * (size_t)n);
+        if (hipGetLastError() != hipSuccess) rc = -3;
+    }
+    if (!rc && hipMemcpy(h_out, d + 3 * (size_t)n, bytes, hipMemcpyDeviceToHost) != hipSuccess) rc = -3;
+    (void)hipFree(d);
+    return rc;
+}

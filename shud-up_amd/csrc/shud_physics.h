@@ -44,13 +44,22 @@ namespace shud {
 // rounds to nearest exactly like IEEE division (Markstein's theorem; round-to-nearest, no under/overflow).
 // Exact, zero, infinite and NaN residuals keep q0 (signed zeros and infinities as a/b gives them).
 // SHUD_CDIV=0 uses the plain division (A/B: identical results, CDIV=1 measured 1 % faster on syn-10M).
+// Range: the handle admits a divisor only when it is 0, +-inf, NaN or 2^-20 <= |b| <= 2^20 (kCdivBmin/Bmax,
+// checked at create); then for 2^-948 <= |a| <= 2^1000 neither q0 nor the residual leaves the normal range and
+// the theorem holds.  Outside that numerator range (tiny non-zero or huge a: subnormal quotients, overflow of
+// a*rb) the exec-masked cold path takes the IEEE division itself, so cdiv(a, b, RN(1/b)) == a / b for every a
+// (tests/test_kat.py::test_cdiv_bit_identical on subnormal, near-overflow, signed-zero and special operands).
+// Zero, infinite and NaN numerators and 0/inf/NaN divisors stay on the fast path: q0 is then already a / b.
 #ifndef SHUD_CDIV
 #define SHUD_CDIV 1
 #endif
 __device__ __forceinline__ double cdiv(double a, double b, double rb) {
     const double q0 = a * rb;
     const double e = __builtin_fma(-q0, b, a);
-    return (e == 0. || !__builtin_isfinite(e)) ? q0 : __builtin_fma(e, rb, q0);
+    double q = (e == 0. || !__builtin_isfinite(e)) ? q0 : __builtin_fma(e, rb, q0);
+    const double aa = __builtin_fabs(a);
+    if (__builtin_expect((aa < 0x1p-948 && a != 0.) || aa > 0x1p1000, 0)) q = a / b;
+    return q;
 }
 #if SHUD_CDIV && !(SHUD_ABL & 8)
 #define CDIV_(a, b, rb) cdiv(a, b, rb)
@@ -73,10 +82,14 @@ __device__ __forceinline__ double rmin(double a, double b) { return (a > b ? b :
 __device__ __forceinline__ double rmax(double a, double b) { return (a < b ? b : a); }
 __device__ __forceinline__ double pow23(double x) { double t = SCBRT(x); return t * t; }
 
-// Equations.hpp:54-63
+// Equations.hpp:54-63.  The reference's two branches differ only in the sqrt argument (S or -S) and a leading
+// -1.0 factor; IEEE multiplication and division round sign-symmetrically, so (-1.0*x)*A*p/n == -(x*A*p/n) bit
+// for bit (zeros and NaNs included).  One sqrt of the selected argument, one chain, a final sign select —
+// the compiler if-converted the two branches into two full sqrt sequences per call otherwise.
 __device__ __forceinline__ double manning(double A, double n, double R, double S) {
-    if (S > 0) return SDIV(SSQRT(S) * A * pow23(R), n);
-    return SDIV(-1.0 * SSQRT(-S) * A * pow23(R), n);
+    const bool pos = S > 0;
+    const double t = SDIV(SSQRT(pos ? S : -S) * A * pow23(R), n);
+    return pos ? t : -t;
 }
 // Equations.cpp:116-134 (range check reported through *bad)
 __device__ __forceinline__ double eff_kh(double ygw, double aq, double macd, double kmac, double af,
@@ -88,37 +101,37 @@ __device__ __forceinline__ double eff_kh(double ygw, double aq, double macd, dou
     return e;
 }
 // MD_RiverFlux.cpp:65-98
+// Both branches evaluate cwr*sqrt(2g*y)*width*y*60 on their own y, the second with a leading -1.0 factor:
+// as in manning() the negation is exact, so one sqrt chain on the selected y and a sign select give the same
+// bits as the two branches (which the compiler otherwise if-converts into two sqrt sequences).
 __device__ __forceinline__ double weir_jtoi(double zi, double yi, double zj, double yj, double zbank,
                                             double cwr, double width, double thr) {
-    double hi = yi + zi, hj = yj + zj, dh = hj - hi, y, Q;
-    if (dh > 0.) {
-        y = hi - zbank;
-        if ((y > 0.) & (yj > thr)) {
-            if (hi > zbank) y = dh;
-            Q = cwr * SSQRT(2. * K_GRAV * y) * width * y * 60.;
-        } else Q = 0.;
-    } else {
-        y = hi - zbank;
-        if (y > 0. && yi > thr) {
-            if (hj > zbank) y = -dh;
-            Q = -1. * cwr * SSQRT(2. * K_GRAV * y) * width * y * 60.;
-        } else Q = 0.;
-    }
-    return Q;
+    const double hi = yi + zi, hj = yj + zj, dh = hj - hi;
+    const bool up = dh > 0.;                         // flow j -> i
+    double y = hi - zbank;
+    const bool on = up ? ((y > 0.) & (yj > thr)) : (y > 0. && yi > thr);
+    if (up ? (hi > zbank) : (hj > zbank)) y = up ? dh : -dh;
+    const double t = cwr * SSQRT(2. * K_GRAV * y) * width * y * 60.;
+    return on ? (up ? t : -t) : 0.;
 }
 // Flux_RiverElement.cpp:11-55
+// RD: D's correctly rounded reciprocal rD is given (cdiv); otherwise the plain division
+template <bool RD = false>
 __device__ __forceinline__ double r2e_gw(double yr, double zr, double ye, double ze, double kele,
-                                         double kriv, double L, double D) {
+                                         double kriv, double L, double D, double rD = 0.) {
     if (kele < K_ZERO || kriv < K_ZERO) return 0.;
     double K = (kele * 1. + kriv * 1.) / (1. + 1.);   // meanArithmetic(k1,k2,1,1) Equations.hpp:50-52
-    double he = ye + ze, hr = yr + zr, dh = hr - he, A, Q = 0.;
-    if (dh > K_ZERO) {
-        A = (he > zr) ? (yr + (he - zr)) * .5 * L : yr * L;
-        Q = (yr < K_EPSILON) ? 0. : A * K * SDIV(dh, D);
-    } else if (dh < -K_ZERO) {
-        if (ye > K_ZERO) { A = (yr + (he - zr)) * .5 * L; Q = A * K * SDIV(dh, D); }
-    }
-    return Q;
+    // both flowing branches evaluate A * K * (dh / D) on their own A: one division, branch-selected A
+    const double he = ye + ze, hr = yr + zr, dh = hr - he;
+    const bool in = dh > K_ZERO;
+    const double A = (in && !(he > zr)) ? yr * L : (yr + (he - zr)) * .5 * L;
+    const bool on = in ? !(yr < K_EPSILON) : (dh < -K_ZERO && ye > K_ZERO);
+    return on ? A * K * (RD ? CDIV_(dh, D, rD) : SDIV(dh, D)) : 0.;
+}
+// x / a for x = 0.0 (QSS, never assigned by the reference): +-0 with a's sign for a non-zero a, NaN for a zero
+// or NaN a — the IEEE quotient, without a division
+__device__ __forceinline__ double zero_over(double a) {
+    return (a != 0. && a == a) ? __builtin_copysign(0.0, a) : __builtin_nan("");
 }
 
 // single-use stream loads: non-temporal when the variant asks for it (VAR bit 1)

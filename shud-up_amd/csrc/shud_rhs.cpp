@@ -332,6 +332,10 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         }
     // identities the packed record relies on (else the SoA kernel runs): AquiferDepth == z_surf - z_bottom
     // (InitElement after rmSinks, Model_Data.cpp:262-264), |iBC| fits int8, <= 63 segments per element
+    // the packed kernel addresses its element / segment streams with 32-bit byte offsets (at(), shud_ele_packed.hip)
+    if ((uint64_t)48 * NE >= (1ull << 32) || (uint64_t)48 * m->num_seg >= (1ull << 32) ||
+        (uint64_t)24 * NE + 8ull * m->num_riv >= (1ull << 32))
+        return 0;
     for (int i = 0; i < NE; i++) {
         if (!(p->aquifer_depth[i] == m->z_surf[i] - m->z_bottom[i])) return 0;
         const int ibc = m->ibc ? m->ibc[i] : 0;
@@ -388,6 +392,10 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         t[CF_kmax] = t[CF_infKsatV] * (1. - t[CF_hAreaF]) + t[CF_macKsatV] * t[CF_hAreaF];
         t[CF_ekA] = t[CF_infKsatV] * (1. - t[CF_hAreaF]);
         t[CF_ekB] = t[CF_hAreaF] * t[CF_macKsatV];
+        // cdiv's range (shud_dev.h cdiv_divisor_ok); otherwise plain divisions in the SoA kernel
+        if (!cdiv_divisor_ok(t[CF_fcmr]) || !cdiv_divisor_ok(t[CF_dTh]) || !cdiv_divisor_ok(t[CF_infD]) ||
+            !cdiv_divisor_ok(t[CF_Sy]))
+            return 0;
         t[CF_r_fcmr] = 1. / t[CF_fcmr];
         t[CF_r_dTh] = 1. / t[CF_dTh];
         t[CF_r_infD] = 1. / t[CF_infD];
@@ -420,6 +428,29 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     if ((rc = h->upload(&sf_d, sfirst.data(), NE))) return rc;
     P.ctab = ctab_d; P.ncls = ncls; P.zz = zz_d; P.meta = meta_d; P.ged = ged_d; P.area = area_d;
     P.seg_first = sf_d;
+    // host reciprocals of static geometric divisors for a kernel built with SHUD_RCP (A/B builds)
+    const int rcp = shud_ele_rcp_mask();
+    if (rcp & 1) {
+        std::vector<double> ra(NE);
+        for (int i = 0; i < NE; i++) {
+            if (!cdiv_divisor_ok(m->area[i])) return 0;
+            ra[i] = 1. / m->area[i];
+        }
+        double *ra_d;
+        if ((rc = h->upload(&ra_d, ra.data(), NE))) return rc;
+        P.r_area = ra_d;
+    }
+    if (rcp & 2) {
+        std::vector<double> rd(3 * (size_t)NE);
+        for (size_t k = 0; k < rd.size(); k++) {
+            const double d = m->dist2nabor[k];
+            if (m->nabr[k] >= 0 && !cdiv_divisor_ok(d)) return 0;      // used on interior and bank edges only
+            rd[k] = 1. / d;
+        }
+        double *rd_d;
+        if ((rc = h->upload(&rd_d, rd.data(), rd.size()))) return rc;
+        P.r_d2n = rd_d;
+    }
     {   // element-sorted segment records with their reach's statics (seg_perm: element-sorted -> reference)
         const int NSg = m->num_seg;
         std::vector<double2> lc(NSg), dk(NSg);
@@ -438,6 +469,16 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         if ((rc = h->upload(&rb_d, rb.data(), NSg))) return rc;
         if ((rc = h->upload(&bt_d, bt.data(), NSg))) return rc;
         P.sg_lc = lc_d; P.sg_dk = dk_d; P.sg_rb = rb_d; P.sg_bt = bt_d;
+        if (rcp & 4) {
+            std::vector<double> rbt(NSg);
+            for (int k = 0; k < NSg; k++) {
+                if (!cdiv_divisor_ok(bt[k])) return 0;
+                rbt[k] = 1. / bt[k];
+            }
+            double *rbt_d;
+            if ((rc = h->upload(&rbt_d, rbt.data(), NSg))) return rc;
+            P.sg_rbt = rbt_d;
+        }
         if ((rc = h->upload(&P.qseg2, (const double2 *)nullptr, NSg))) return rc;
     }
     if ((rc = h->upload(&P.s_np, (const double2 *)nullptr, NE))) return rc;
@@ -467,37 +508,49 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         h->rseg_perm = rorder;
     }
     std::vector<double2> rv(4 * (size_t)NR);
-    std::vector<int4> ri(NR), ru(NR);
     const int nor = h->n_own_riv;
+    std::vector<int4> ri(nor);
+    std::vector<double2> rdn(2 * (size_t)nor), upr(4 * (size_t)up_off[nor]);
+    auto pack_ib = [](int a, int b) {                        // two int32 in one double slot
+        double v;
+        const int32_t two[2] = {a, b};
+        memcpy(&v, two, sizeof v);
+        return v;
+    };
+    auto down_of = [&](int r) { return (h->lakeon && m->riv_down[r] <= -4) ? -3 : m->riv_down[r]; };  // lake: outlet
+    auto bc_of = [&](int r) { return m->riv_bc ? m->riv_bc[r] : 0; };
     for (int r = 0; r < NR; r++) {
-        const int dn = (h->lakeon && m->riv_down[r] <= -4) ? -3 : m->riv_down[r];   // into a lake: outlet formula
-        const int bc = m->riv_bc ? m->riv_bc[r] : 0;
-        double ib;                                                   // (down, BC) packed into the 4th slot
-        const int32_t two[2] = {dn, bc};
-        memcpy(&ib, two, sizeof ib);
         rv[4 * (size_t)r + 0] = make_double2(m->riv_bottom_width[r], m->riv_bankslope[r]);
         rv[4 * (size_t)r + 1] = make_double2(m->riv_length[r], m->riv_bed_slope[r]);
         rv[4 * (size_t)r + 2] = make_double2(m->riv_dist2down[r], m->riv_avg_rough[r]);
-        rv[4 * (size_t)r + 3] = make_double2(m->riv_depth[r], ib);
-        ri[r] = make_int4(dn, bc, rstart[r], rcnt[r]);
-        int4 u = make_int4(0, 0, 0, 0);
-        if (r < nor) {
-            const int n = up_off[r + 1] - up_off[r];
-            if (n <= 3) {
-                int v[3] = {0, 0, 0};
-                for (int k = 0; k < n; k++) v[k] = up_idx[up_off[r] + k];
-                u = make_int4(v[0], v[1], v[2], n);
-            } else {
-                u = make_int4(0, 0, 0, -1);
-            }
-        }
-        ru[r] = u;
+        rv[4 * (size_t)r + 3] = make_double2(m->riv_depth[r], pack_ib(down_of(r), bc_of(r)));
     }
-    double2 *rv_d; int4 *ri_d, *ru_d;
+    // owned reaches: segment range, upstream CSR, and the downstream / upstream QrivDown statics (same
+    // expressions and order as the kernel computed them: smean = (slope + slope_down) * 0.5; -ffp-contract=off)
+    for (int r = 0; r < nor; r++) {
+        ri[r] = make_int4(rstart[r], rcnt[r], up_off[r], up_off[r + 1] - up_off[r]);
+        const int dn = down_of(r);
+        const int d = dn >= 0 ? dn : r;                      // outlets: harmless self load
+        if (dn >= 0 && !cdiv_divisor_ok(m->riv_dist2down[r])) return 0;
+        rdn[2 * (size_t)r] = make_double2(dn >= 0 ? (m->riv_bed_slope[r] + m->riv_bed_slope[d]) * 0.5 : 0.,
+                                          dn >= 0 ? m->riv_depth[d] : 0.);
+        rdn[2 * (size_t)r + 1] = make_double2(dn >= 0 ? 1. / m->riv_dist2down[r] : 0., pack_ib(d, bc_of(d)));
+        for (int k = up_off[r]; k < up_off[r + 1]; k++) {
+            const int u = up_idx[k];
+            if (!cdiv_divisor_ok(m->riv_dist2down[u])) return 0;
+            upr[4 * (size_t)k + 0] = make_double2(m->riv_bottom_width[u], m->riv_bankslope[u]);
+            upr[4 * (size_t)k + 1] = make_double2(m->riv_depth[u], m->riv_dist2down[u]);
+            upr[4 * (size_t)k + 2] = make_double2(m->riv_avg_rough[u], (m->riv_bed_slope[u] + m->riv_bed_slope[r]) * 0.5);
+            upr[4 * (size_t)k + 3] = make_double2(pack_ib(u, bc_of(u)), 1. / m->riv_dist2down[u]);
+        }
+    }
+    double2 *rv_d, *rdn_d, *upr_d; int4 *ri_d;
     if ((rc = h->upload(&rv_d, rv.data(), rv.size()))) return rc;
-    if ((rc = h->upload(&ri_d, ri.data(), NR))) return rc;
-    if ((rc = h->upload(&ru_d, ru.data(), NR))) return rc;
-    P.rv = rv_d; P.rv_i = ri_d; P.rv_u = ru_d;
+    // (at least one entry each, zero-filled when empty, so the device pointers are never null)
+    if ((rc = h->upload(&ri_d, ri.empty() ? nullptr : ri.data(), std::max<size_t>(ri.size(), 1)))) return rc;
+    if ((rc = h->upload(&rdn_d, rdn.empty() ? nullptr : rdn.data(), std::max<size_t>(rdn.size(), 1)))) return rc;
+    if ((rc = h->upload(&upr_d, upr.empty() ? nullptr : upr.data(), std::max<size_t>(upr.size(), 1)))) return rc;
+    P.rv = rv_d; P.rv_i = ri_d; P.rv_dn = rdn_d; P.upr = upr_d;
     h->n_classes = ncls;
     h->packed = true;
     return 0;
@@ -611,10 +664,12 @@ static int setup_partition(shud_rhs *h, const ShudPartition *part) {
         memcpy(&id, part->nccl_unique_id, sizeof(id));
         h->use_nccl = true;
         NCCL_TRY(ncclCommInitRank(&h->comm, P, id, part->rank));
-        HIP_TRY(hipStreamCreateWithFlags(&h->s_comm, hipStreamNonBlocking));
-        HIP_TRY(hipEventCreateWithFlags(&h->ev_pack, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&h->ev_comm, hipEventDisableTiming));
     }
+    // the pack kernel and the exchange run on a side stream beside the interior element kernel (RCCL and
+    // external transport alike, so the one-GPU rank timings measure the same pipeline)
+    HIP_TRY(hipStreamCreateWithFlags(&h->s_comm, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&h->ev_pack, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&h->ev_comm, hipEventDisableTiming));
     return 0;
 }
 
@@ -721,18 +776,18 @@ extern "C" int shud_rhs_set_step_inputs(shud_rhs_t h, const ShudStepInputs *in) 
 // ---------------------------------------------------------------------------------------------
 // eval
 // ---------------------------------------------------------------------------------------------
-// pack the owned states peers need (main stream), then the grouped RCCL send/recv on the comm stream:
-// ev_comm marks the ghost buffers filled.
+// on the comm stream, once y is ready on the main stream (ev_pack): pack the owned states peers need, then the
+// grouped RCCL send/recv; ev_comm marks the ghost buffers filled.  The main stream meanwhile runs the interior
+// elements, so the pack (~4 us at 8 ranks) and the exchange leave the critical path.  s_comm is in order and
+// waits for everything enqueued on the main stream before this eval, so neither the send buffers nor the
+// ghost buffers are rewritten while the previous eval still reads them.
 static int exchange(shud_rhs *h, const double *y) {
     if (!h->partitioned) return 0;
-    // SHUD_RHS_NOPACK=1: timing ablation for external transport only (tools/rank_timing.py): no pack kernel
-    static const bool nopack = [] { const char *e = getenv("SHUD_RHS_NOPACK"); return e && e[0] == '1'; }();
-    if (nopack && !h->use_nccl) return 0;
-    launch_pack_kernel(y, h->n_own, h->n_own_riv, h->d_esend_idx, h->n_esend, h->d_rsend_idx, h->n_rsend,
-                       h->d_esend, h->d_rsend, h->stream);
-    if (!h->use_nccl) return 0;      // external transport (tests): caller moved the buffers
     HIP_TRY(hipEventRecord(h->ev_pack, h->stream));
     HIP_TRY(hipStreamWaitEvent(h->s_comm, h->ev_pack, 0));
+    launch_pack_kernel(y, h->n_own, h->n_own_riv, h->d_esend_idx, h->n_esend, h->d_rsend_idx, h->n_rsend,
+                       h->d_esend, h->d_rsend, h->s_comm);
+    if (h->use_nccl) {
     NCCL_TRY(ncclGroupStart());
     for (int p = 0; p < h->nranks; p++) {
         if (p == h->rank) continue;
@@ -744,6 +799,7 @@ static int exchange(shud_rhs *h, const double *y) {
         if (rr) NCCL_TRY(ncclRecv(h->d_griv + h->rrecv_off[p], rr, ncclDouble, p, h->comm, h->s_comm));
     }
     NCCL_TRY(ncclGroupEnd());
+    }                                // external transport (tests): the caller placed the ghost buffers
     HIP_TRY(hipEventRecord(h->ev_comm, h->s_comm));
     return 0;
 }
@@ -754,7 +810,8 @@ static void launch_ele(shud_rhs *h, const double *y, double *dy, int cur, int cu
     if (i1 < 0) i1 = h->n_own + h->n_segghost;
     if (h->packed && !h->variant)
         launch_element_kernel_packed(h->dm, h->dp, Y, dy, i0, i1, cur, h->mode, h->open, diag,
-                                     h->fu_unit[0] && h->fu_unit[1], h->dd, h->stream, h->lakeon ? &h->lk : nullptr);
+                                     h->fu_unit[0] && h->fu_unit[1], h->dd, h->stream, h->lakeon ? &h->lk : nullptr,
+                                     h->partitioned && i1 <= h->n_int);
     else
         launch_element_kernel(h->dm, Y, dy, h->n_own + h->n_segghost, cur, cur_e, h->mode, h->open, diag, h->dd,
                               h->stream, h->variant);
@@ -796,17 +853,19 @@ static const uint32_t kFatal = SHUD_EF_NAN_QELE | SHUD_EF_EFFKH | SHUD_EF_ET_NEG
 
 // partitioned handles: the interior elements [0, n_int) run while the halo exchange is in flight (RCCL on
 // s_comm); boundary + ghost elements and the reaches wait for it.  Unpartitioned: one launch each.
+// SHUD_ABL_NOSPLIT (timing-only build, tools/rank_timing.py ablations): one element launch after the exchange
+#ifndef SHUD_ABL_NOSPLIT
+#define SHUD_ABL_NOSPLIT 0
+#endif
 static int launch_split(shud_rhs *h, const double *y, double *dy, hipEvent_t e_mid = nullptr) {
-    // SHUD_RHS_NOSPLIT=1: timing ablation (tools/rank_timing.py): one element launch after the exchange
-    static const bool nosplit = [] { const char *e = getenv("SHUD_RHS_NOSPLIT"); return e && e[0] == '1'; }();
-    if (h->partitioned && h->packed && !h->variant && h->n_int > 0 && !nosplit) {
+    if (h->partitioned && h->packed && !h->variant && h->n_int > 0 && !SHUD_ABL_NOSPLIT) {
         launch_ele(h, y, dy, h->cur, h->cur_e, false, 0, h->n_int);
-        if (h->use_nccl) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_comm, 0));
+        HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_comm, 0));
         launch_ele(h, y, dy, h->cur, h->cur_e, false, h->n_int, h->n_own + h->n_segghost);
         if (e_mid) HIP_TRY(hipEventRecord(e_mid, h->stream));
         launch_riv(h, y, dy, false);
     } else {
-        if (h->use_nccl) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_comm, 0));
+        if (h->partitioned) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_comm, 0));
         launch_ele(h, y, dy, h->cur, h->cur_e, false);
         if (e_mid) HIP_TRY(hipEventRecord(e_mid, h->stream));
         launch_riv(h, y, dy, false);
@@ -1055,6 +1114,7 @@ extern "C" int shud_rhs_eval_pack(shud_rhs_t h, const double *d_y) {
     launch_pack_kernel(d_y, h->n_own, h->n_own_riv, h->d_esend_idx, h->n_esend, h->d_rsend_idx, h->n_rsend,
                        h->d_esend, h->d_rsend, h->stream);
     HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(h->ev_comm, h->stream));      // what eval_compute's boundary launch waits for
     return SHUD_OK;
 }
 extern "C" int shud_rhs_eval_compute(shud_rhs_t h, double t, const double *d_y, double *d_ydot) {
@@ -1126,7 +1186,7 @@ extern "C" int shud_rhs_time_kernels(shud_rhs_t h, double t, const double *d_y, 
         if (h->partitioned) {
             int rc = exchange(h, d_y);        // serialized here (no overlap) so each phase is timed alone
             if (rc) return rc;
-            if (h->use_nccl) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_comm, 0));
+            HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_comm, 0));
             HIP_TRY(hipEventRecord(E[k++], h->stream));
         }
         launch_ele(h, d_y, d_ydot, h->cur, h->cur_e, false);

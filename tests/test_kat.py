@@ -189,3 +189,69 @@ def test_pow_pos_bit_identical():
     assert lib.shud_kat_pow(1, xy.ctypes.data, m, fast.ctypes.data) == 0
     same = full.view(np.uint64) == fast.view(np.uint64)
     assert same.all(), f"{(~same).sum()} differ, first (x, y) = {xy[np.argmax(~same)]}"
+
+
+def _cdiv_operands():
+    """(a, b) pairs for cdiv: divisors in the handle's admitted range [2^-20, 2^20] plus 0 / inf / NaN (the
+    class constants a model may carry), numerators across the whole double range with the guard boundaries
+    2^-948 / 2^1000, subnormals, DBL_MAX, signed zeros, infinities and NaN."""
+    rng = np.random.default_rng(2024)
+    n = 1 << 18
+    b = np.concatenate([np.exp2(rng.uniform(-20, 20, n)) * rng.choice([-1.0, 1.0], n),
+                        rng.uniform(1e-3, 1e4, n),
+                        np.array([2.0 ** -20, 2.0 ** 20, 1.0, 3.0, 0.1, 0.3, 0.0, -0.0, np.inf, -np.inf, np.nan])])
+    m = b.size
+    e = rng.uniform(-1074, 1024, m)
+    a = np.exp2(np.clip(e, -1074, 1023.999)) * rng.choice([-1.0, 1.0], m)
+    # boundary bands: just below/above the guard thresholds and at the subnormal / overflow edges
+    band = rng.integers(0, 6, m)
+    a = np.where(band == 0, np.exp2(rng.uniform(-952, -944, m)), a)
+    a = np.where(band == 1, np.exp2(rng.uniform(996, 1004, m)) * rng.uniform(1, 1.999, m), a)
+    a = np.where(band == 2, rng.integers(1, 1 << 52, m).astype(np.uint64).view(np.float64), a)   # subnormals
+    a = np.where(band == 3, np.finfo(np.float64).max * rng.uniform(0.5, 1.0, m), a)
+    specials = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 5e-324, -5e-324, 2.0 ** -948, 2.0 ** 1000,
+                         np.nextafter(2.0 ** -948, 0), np.nextafter(2.0 ** 1000, np.inf), np.finfo(np.float64).max])
+    sa, sb = np.meshgrid(specials, b[-11:])
+    a = np.concatenate([a, sa.ravel()])
+    b = np.concatenate([b, sb.ravel()])
+    return np.ascontiguousarray(a), np.ascontiguousarray(b)
+
+
+def _bits_same(got, want):
+    return (got.view(np.uint64) == want.view(np.uint64)) | (np.isnan(got) & np.isnan(want))
+
+
+def test_cdiv_algorithm_bit_identical(tmp_path):
+    """The reciprocal division cdiv (shud_physics.h: q0 = a*RN(1/b), one fma residual, one fma correction;
+    IEEE division on the cold path for 0 < |a| < 2^-948 or |a| > 2^1000) restated in C with glibc's correctly
+    rounded fma equals IEEE a / b bit for bit on the admitted divisors — subnormal quotients and overflow
+    included — while the unguarded form does not (Markstein needs no under/overflow)."""
+    import subprocess
+    so = str(tmp_path / "libcdiv.so")
+    subprocess.check_call(["gcc", "-O2", "-ffp-contract=off", "-fno-fast-math", "-shared", "-fPIC", "-o", so,
+                           os.path.join(os.path.dirname(__file__), "cdiv_emul.c"), "-lm"])
+    lib = C.CDLL(so)
+    lib.cdiv_eval.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+    a, b = _cdiv_operands()
+    with np.errstate(all="ignore"):
+        want = a / b
+    got, raw = np.zeros_like(a), np.zeros_like(a)
+    lib.cdiv_eval(a.ctypes.data, b.ctypes.data, a.size, 1, got.ctypes.data)
+    lib.cdiv_eval(a.ctypes.data, b.ctypes.data, a.size, 0, raw.ctypes.data)
+    ok = _bits_same(got, want)
+    assert ok.all(), f"{(~ok).sum()} differ, first (a, b) = {a[np.argmax(~ok)]!r}, {b[np.argmax(~ok)]!r}"
+    assert not _bits_same(raw, want).all()          # the guard is needed: the raw form misses subnormal cases
+
+
+@pytest.mark.gpu
+def test_cdiv_bit_identical():
+    """The device cdiv with the host's reciprocal equals IEEE a / b bit for bit on the same operands."""
+    lib = C.CDLL(os.path.join(PKG_DIR, "libshud_kat.so"))
+    lib.shud_kat_cdiv.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+    a, b = _cdiv_operands()
+    with np.errstate(all="ignore"):
+        want = a / b
+    got = np.zeros_like(a)
+    assert lib.shud_kat_cdiv(a.ctypes.data, b.ctypes.data, a.size, got.ctypes.data) == 0
+    ok = _bits_same(got, want)
+    assert ok.all(), f"{(~ok).sum()} differ, first (a, b) = {a[np.argmax(~ok)]!r}, {b[np.argmax(~ok)]!r}"

@@ -1,0 +1,47 @@
+#!/bin/bash
+# GPU box: one parameterised step runner for every gpurun call (replaces the per-call gNN.sh files).
+#   bash tools/gpu_run.sh OUTDIR STEP [STEP ...]
+# steps (each under its own timeout; the first failure ends the call):
+#   suite        pytest -m gpu (full), log + durations        smoke     __graft_entry__.smoke()
+#   bench        the driver's command: bench.py --gpus 1 --steps 20 --warmup 5
+#   quick        RHS-only bench line (no CPU baseline / ET / integrator / e2e)
+#   ab:L1,L2     tools/ab_variants.py on the production lib and each build/ab/libshud_rhs_<L>.so
+#   kt           rocprofv3 kernel trace of the RHS-only bench            pmc   FETCH_SIZE / WRITE_SIZE passes -> summary
+#   sq           SQ / GRBM counter passes (tools/sq_counters.sh)          ode   integrator kernel trace
+#   part1        bench's N>1 code path on one rank                        rank  tools/rank_timing.py (2/4/8-way)
+#   e2e          tools/profile_e2e.sh 1M, 1 day
+#   test:EXPR    pytest -m gpu -k EXPR
+set -e
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=$1; shift
+mkdir -p "$O"
+A="--no-cpu-baseline --no-et --no-ode --no-many-class --no-host-vectors --e2e-ele 0"
+for step in "$@"; do
+  echo "[$(date +%T)] $step"
+  case "$step" in
+    suite) timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --durations=30 --timeout 240 --timeout-method thread > "$O/pytest_gpu.log" 2>&1 ;;
+    test:*) timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread -k "${step#test:}" > "$O/pytest_sel.log" 2>&1 ;;
+    smoke) timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 ;;
+    bench) timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > "$O/bench.json" 2> "$O/bench.err" ;;
+    quick) timeout -k 10 300 python bench.py $A --steps 20 --warmup 5 > "$O/quick.json" 2> "$O/quick.err" ;;
+    ab:*)
+      libs="${step#ab:}"
+      timeout -k 10 300 python tools/ab_variants.py --variants pk --rounds 5 > "$O/ab_prod.log" 2>&1
+      for n in ${libs//,/ }; do
+        SHUD_RHS_LIB=$PWD/shud-up_amd/build/ab/libshud_rhs_$n.so timeout -k 10 300 python tools/ab_variants.py --variants pk --rounds 5 > "$O/ab_$n.log" 2>&1
+      done
+      for f in prod ${libs//,/ }; do echo "$f $(tail -n 1 "$O/ab_$f.log")"; done > "$O/ab_summary.log" ;;
+    kt) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt" -o run -- python3 bench.py $A --steps 20 --warmup 5 > "$O/bench_kt.json" 2> "$O/bench_kt.err" ;;
+    pmc)
+      timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch" -o run -- python3 bench.py $A --steps 5 --warmup 1 > "$O/pmc_fetch.log" 2>&1
+      timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_write" -o run -- python3 bench.py $A --steps 5 --warmup 1 > "$O/pmc_write.log" 2>&1
+      python3 tools/pmc_summary.py "$O/pmc_fetch" "$O/pmc_write" 10001406 "$O/pmc_summary.json" > /dev/null ;;
+    sq) timeout -k 10 400 bash tools/sq_counters.sh "$O" > /dev/null ;;
+    ode) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt_ode" -o run -- python3 bench.py --no-cpu-baseline --no-et --no-many-class --no-host-vectors --e2e-ele 0 --steps 5 --warmup 1 > "$O/bench_ode_kt.json" 2> "$O/bench_ode_kt.err" ;;
+    part1) timeout -k 10 300 python bench.py $A --partition-1 --steps 20 > "$O/bench_partition1.json" 2> "$O/bench_partition1.err" ;;
+    rank) timeout -k 10 400 python tools/rank_timing.py > "$O/rank_timing.json" 2> "$O/rank_timing.err" ;;
+    e2e) timeout -k 10 600 bash tools/profile_e2e.sh 1000000 1 > "$O/e2e.log" 2>&1 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo done
