@@ -109,11 +109,13 @@ int shud_out_add(shud_out_t o, const ShudPrintSpec *spec);
  * finished interval reach the files asynchronously (copy stream + writer thread; same bytes, same order):
  * shud_out_flush / shud_out_rows / shud_out_destroy wait for them. */
 int shud_out_export(shud_out_t o, double t);
-/* wait until every exported row is written to the files (fflush'ed) */
+/* wait until every exported row is written to the files (fflush'ed).  Returns the first failure of the
+ * asynchronous writer (a failed snapshot copy: that row is not written; a file write / flush error) */
 int shud_out_flush(shud_out_t o);
-/* number of rows written so far by control k (tests; waits for the writer) */
+/* number of rows written so far by control k (tests; waits for the writer); a writer failure returns its
+ * negative SHUD_ERR_* code */
 int64_t shud_out_rows(shud_out_t o, int k);
-/* flushes and closes the files, frees the buffers */
+/* flushes and closes the files, frees the buffers; returns the writer's first failure, if any */
 int shud_out_destroy(shud_out_t o);
 
 #ifdef __cplusplus

@@ -92,7 +92,8 @@ struct DevPacked {
                             //   (zz and meta.w are neighbour-gathered)
     const double2 *ged;     // [3][NE] edge-major {edge_j, dist2nabor_j}
     const double *area;
-    const int *seg_first;   // first element-sorted segment of each element
+    int *seg_first;         // bits 0-30: first element-sorted segment of the element; bit 31: t_lai > ZERO
+                            //   (f_etFlux's only use of LAI, MD_ET.cpp:381; rewritten with the step inputs)
     const double2 *sg_lc;   // [NS] element-sorted segments: {length, Cwr}
     const double2 *sg_dk;   //   its reach's {depth, KsatH}
     const int2 *sg_rb;      //   {reach, reach BC column}
@@ -101,7 +102,7 @@ struct DevPacked {
                             //   reach-sorted when seg_rpos is set)
     const int *seg_rpos;    // nullptr, or element-sorted k -> reach-sorted slot (SHUD_RHS_SEG_ORDER=reach)
     double2 *s_np;          // {net_prep, pot_evap}        step inputs (packed by shud_pack_step_kernel)
-    double2 *s_tl;          // {pot_tran, lai}
+    double2 *s_tl;          // {pot_tran, ETP} (ETP: the eta > 2*ETP warning, MD_ET.cpp:391)
     double2 *s_fu;          // {fu_surf, fu_sub}            read only when not all ones
     double2 *cs[2];         // carried {u_satn, qEleE_IC}, ping-pong
     // reaches (owned first): 16-byte records
@@ -109,15 +110,8 @@ struct DevPacked {
     // depth, (down, BC)}: everything a reach's own, its downstream's and its upstream reaches' QrivDown read,
     // so a neighbour reach costs one cache line instead of one line per field pair
     const double2 *rv;      // [4 * NR]
-    const int4 *rv_i;       // owned reaches: {first reach-sorted segment, #segments, first upstream record, #up}
-    // owned reaches: the downstream term's statics, 32 B {smean = (slope + slope_down) * 0.5, depth_down |
-    // RN(1/Dist2DownStream), (down or self, BC of down)} — the downstream reach costs its 8-B stage only
-    const double2 *rv_dn;   // [2 * n_own_riv]
-    // one 64-B record per (owned reach, upstream reach), CSR in ascending (global) upstream order (MD_f.cpp:
-    // 236-240): the upstream reach's QrivDown statics {BottomWidth, bankslope | depth, Dist2DownStream |
-    // avgRough, smean = (slope_u + slope) * 0.5 | (u, BC_u), RN(1/Dist2DownStream_u)} — contiguous per reach
-    // instead of one scattered 64-B line per upstream reach
-    const double2 *upr;     // [4 * #upstream edges]
+    const int4 *rv_i;       // {down, BC, first reach-sorted segment, #segments}
+    const int4 *rv_u;       // {up0, up1, up2, #up} (ascending global order); #up = -1: use up_off/up_idx
     // correctly rounded reciprocals of static geometric divisors, uploaded only for a kernel built with the
     // matching SHUD_RCP bit (shud_ele_rcp_mask()): 1 area, 2 Dist2Nabor [3][NE], 4 segment reach BedThick
     const double *r_area, *r_d2n, *sg_rbt;

@@ -118,8 +118,8 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     const int cf = mt.w;
     const int cid = cf_class(cf), ibc = cf_ibc(cf);
     const bool is_lake = LAKE && cf < 0;
-    const double2 snp = ldnt2(at(p.s_np, o16)), stl = ldnt2(at(p.s_tl, o16));
-    const double etp = ldnt(at(m.etp, o8));
+    const double2 snp = ldnt2(at(p.s_np, o16)), stl = ldnt2(at(p.s_tl, o16));   // stl = {pot_tran, ETP}
+    const double etp = stl.y;
     double2 fu;
     if (FU1) { fu.x = 1.0; fu.y = 1.0; } else fu = ldnt2(at(p.s_fu, o16));
     const double2 csv = ldnt2(at(p.cs[cur], o16));
@@ -151,7 +151,9 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         }
     }
 
-    const int sfirst = *at(p.seg_first, (uint32_t)i << 2);
+    const int sfl = *at(p.seg_first, (uint32_t)i << 2);
+    const int sfirst = sfl & 0x7fffffff;
+    const bool lai_on = sfl < 0;                       // bit 31: t_lai > ZERO (set with the step inputs)
     const int iss = cf_iss(cf), nseg = cf_nseg(cf);
     const double infD = CL(infD), ThR = CL(ThetaR);
     const double infK = CL(infKsatV);
@@ -173,7 +175,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
             if (ugw > aq - infD) { Eg = rmin(rmax(0., ugw), pet - Es) * pj * vb; Eu = 0.; }
             else { Eg = 0.; Eu = rmin(rmax(0., uus), ibeta * (pet - Es)) * pj * vb; }
         }
-        if (stl.y > K_ZERO) {
+        if (lai_on) {                                                // LAI > ZERO
             if (eic >= ptr) { Tg = Tu = 0.; eic = ptr * pj * va; }
             else if (ugw > aq - CL(RzD)) { Tg = rmin(rmax(0., ugw), (ptr - eic)) * pj * va; Tu = 0.; }
             else { Tg = 0.; Tu = rmin(rmax(0., uus), ibeta * (ptr - eic)) * pj * va; }
@@ -416,14 +418,12 @@ __device__ __forceinline__ double riv_stage_p(const DevMesh &m, const YView &Y, 
     *yg = yr;
     return bc > 0 ? m.rybc[bc] : yr;
 }
-// MD_RiverFlux.cpp:5-63: QrivDown of reach q with stage uq and geometry g.  Towards a downstream reach (down >= 0)
-// the slope term is ((uq - depth) - (ud - ddepth)) / Dist2DownStream + smean with the host's smean = (slope +
-// slope_down) * 0.5 (same operations, same order) and the division through cdiv with the host reciprocal
-// rd2d (bit-identical, shud_physics.h); outlets as before.
+// MD_RiverFlux.cpp:5-63: reach q with stage uq and geometry g; its downstream has stage ud, depth, slope
 __device__ __forceinline__ double riv_down_p(const RivP &q, double uq, const RivGeom &g, double ud, double ddepth,
-                                             double smean, double rd2d) {
+                                             double dslope) {
     if (q.down >= 0) {
-        const double s = CDIV_((uq - q.depth) - (ud - ddepth), q.d2d, rd2d) + smean;
+        const double smean = (q.slope + dslope) * 0.5;
+        const double s = ((uq - q.depth) - (ud - ddepth)) / q.d2d + smean;
         const double R = (g.csperem <= K_ZERO) ? 0. : (g.csarea / g.csperem);
         return manning(g.csarea, q.n, R, s);
     } else if (q.down >= -3) {
@@ -435,7 +435,7 @@ __device__ __forceinline__ double riv_down_p(const RivP &q, double uq, const Riv
 }
 // outlet form only (a reach flowing into a lake, the lake kernel's QLakeRivIn: down = -3 on the record)
 __device__ __forceinline__ double riv_down_outlet(const RivP &q, double uq, const RivGeom &g) {
-    return riv_down_p(q, uq, g, 0., 0., 0., 0.);
+    return riv_down_p(q, uq, g, 0., 0., 0.);
 }
 
 // ABL (timing-only ablation builds, -DSHUD_RIV_ABL=k; results are wrong when != 0): bit 0 skips the upstream
@@ -446,36 +446,48 @@ __device__ __forceinline__ double riv_down_outlet(const RivP &q, double uq, cons
 template <int MODE, bool DIAG, int ABL = 0>
 __global__ void __launch_bounds__(256)
 shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, DevDiag dg) {
-    // XCD-chunked workgroup order: neighbouring reaches' segment fluxes and stages share an XCD's L2 (speed only)
+    // XCD-chunked workgroup order: a reach's up/downstream records sit a few blocks away in index space,
+    // so they are L2 hits on the same XCD instead of fabric round trips (speed only)
     const int r = block_id<1>() * blockDim.x + threadIdx.x;
     if (r >= Y.n_own_riv) return;
     const RivP q = riv_load(p, r);
-    const int4 ii = p.rv_i[r];                                  // {first segment, #segments, first up, #up}
-    const double2 dn0 = p.rv_dn[2 * (size_t)r], dn1 = p.rv_dn[2 * (size_t)r + 1];
+    const int4 ii = p.rv_i[r];                                  // {down, BC, first segment, #segments}
+    const int4 up = p.rv_u[r];
     double yg;
     const double ur = riv_stage_p<MODE>(m, Y, r, q.bc, &yg);
     const RivGeom g = riv_geom_p(q, yg);
     double qdown = 0.;
     if (!(ABL & 4)) {
-        const int2 db = rv_ib(dn1.y);                           // (down or self, BC of down): unconditional load
+        const int d = q.down >= 0 ? q.down : r;                 // clamped: unconditional loads
+        const double2 bd = p.rv[4 * (size_t)d + 1], dd = p.rv[4 * (size_t)d + 3];   // same line of d's record
+        const int bcd = rv_ib(dd.y).y;
         double ydg;
-        const double ud = riv_stage_p<MODE>(m, Y, db.x, db.y, &ydg);
-        qdown = riv_down_p(q, ur, g, ud, dn0.y, dn0.x, dn1.x);
+        const double ud = riv_stage_p<MODE>(m, Y, d, bcd, &ydg);
+        qdown = riv_down_p(q, ur, g, ud, dd.x, bd.y);
     }
-    // junction: QrivUp[down] += -QrivDown[i], i ascending (MD_f.cpp:236-240).  Each upstream reach's QrivDown
-    // (towards this reach) from its contiguous record and its 8-B stage
+    // junction: QrivUp[down] += -QrivDown[i], i ascending (MD_f.cpp:236-240)
     double qup = 0.;
-    const int nup = (ABL & 1) ? 0 : ii.w;
-    for (int k = ii.z, k1 = ii.z + nup; k < k1; k++) {
-        const double2 *u4 = p.upr + 4 * (size_t)k;
-        const double2 a = u4[0], b = u4[1], c = u4[2], d = u4[3];
-        const int2 ub = rv_ib(d.x);
-        double yu;
-        const double uu = riv_stage_p<MODE>(m, Y, ub.x, ub.y, &yu);
-        const RivGeom gu = riv_geom(a.x, a.y, 0., yu);
-        const double s = CDIV_((uu - b.x) - (ur - q.depth), b.y, d.y) + c.y;
-        const double R = (gu.csperem <= K_ZERO) ? 0. : (gu.csarea / gu.csperem);
-        qup += -manning(gu.csarea, c.x, R, s);
+    const int nup = (ABL & 1) ? 0 : up.w;
+    if (nup >= 0) {
+        const int uv[3] = {up.x, up.y, up.z};
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            if (k < nup) {
+                const int u = uv[k];
+                const RivP qu = riv_load(p, u);
+                double yu;
+                const double uu = riv_stage_p<MODE>(m, Y, u, qu.bc, &yu);
+                qup += -riv_down_p(qu, uu, riv_geom_p(qu, yu), ur, q.depth, q.slope);
+            }
+        }
+    } else {
+        for (int k = m.up_off[r], k1 = m.up_off[r + 1]; k < k1; k++) {
+            const int u = m.up_idx[k];
+            const RivP qu = riv_load(p, u);
+            double yu;
+            const double uu = riv_stage_p<MODE>(m, Y, u, qu.bc, &yu);
+            qup += -riv_down_p(qu, uu, riv_geom_p(qu, yu), ur, q.depth, q.slope);
+        }
     }
     // segment sums, ascending reference segment order (MD_f.cpp:228-235), gathered from the element-sorted
     // fluxes (scattered 8-B writes from the element kernel cost more than these gathers).  Batches of 8:
@@ -483,13 +495,13 @@ shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     double qsurf = 0., qsub = 0.;
     if (ABL & 2) {
     } else if (p.seg_rpos) {                            // reach-sorted fluxes: this reach's segments are contiguous
-        for (int k = ii.x, k1 = ii.x + ii.y; k < k1; k++) {
+        for (int k = ii.z, k1 = ii.z + ii.w; k < k1; k++) {
             const double2 q2 = p.qseg2[k];
             qsurf += q2.x;
             qsub += q2.y;
         }
     } else
-    for (int k0 = ii.x, k1 = ii.x + ii.y; k0 < k1; k0 += 8) {
+    for (int k0 = ii.z, k1 = ii.z + ii.w; k0 < k1; k0 += 8) {
         int ps[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) ps[j] = m.rseg_pos[k0 + j < k1 ? k0 + j : k0];
@@ -625,7 +637,10 @@ shud_pack_step_kernel(DevMesh m, DevPacked p, int n, int cur, unsigned what) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     if (what & 1) p.s_np[i] = make_double2(m.net_prep[i], m.pot_evap[i]);
-    if (what & 2) p.s_tl[i] = make_double2(m.pot_tran[i], m.lai[i]);
+    if (what & 2) {
+        p.s_tl[i] = make_double2(m.pot_tran[i], m.etp[i]);
+        p.seg_first[i] = (p.seg_first[i] & 0x7fffffff) | (m.lai[i] > K_ZERO ? (int)0x80000000u : 0);
+    }
     if (what & 4) p.s_fu[i] = make_double2(m.fu_surf[i], m.fu_sub[i]);
     if (what & 8) p.cs[cur][i].x = m.u_satn[0][i];
     if (what & 16) p.cs[cur][i].y = m.e_ic[0][i];

@@ -193,6 +193,7 @@ extern "C" int shud_et_step(shud_rhs_t h, const ShudEtForcing *f) {
     d.packed = h->packed ? 1 : 0;
     if (h->packed) {
         d.s_np = h->dp.s_np; d.s_tl = h->dp.s_tl; d.s_fu = h->dp.s_fu; d.cs_cur = h->dp.cs[h->cur];
+        d.sfl = h->dp.seg_first;
     }
     launch_et_kernel(e, d, h->d_err, h->stream);
     HIP_TRY(hipGetLastError());

@@ -211,7 +211,8 @@ __global__ void __launch_bounds__(256) shud_et_kernel(DevEt e, EtStepDev s, DevE
     e.q_eic[i] = eic; e.fu_surf[i] = fu_surf; e.fu_sub[i] = fu_sub;
     if (s.packed) {                                   // the element kernel's records (shud_dev.h DevPacked)
         s.s_np[i] = make_double2(netp, qpet);
-        s.s_tl[i] = make_double2(qptr, lai);
+        s.s_tl[i] = make_double2(qptr, etp);
+        s.sfl[i] = (s.sfl[i] & 0x7fffffff) | (lai > K_ZERO ? (int)0x80000000u : 0);   // f_etFlux's LAI test
         if (s.cryosphere) s.s_fu[i] = make_double2(fu_surf, fu_sub);
         s.cs_cur[i].y = eic;
     }

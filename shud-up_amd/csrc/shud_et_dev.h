@@ -30,6 +30,7 @@ struct EtStepDev {                   // per ET step (uniform across threads)
     double ft_surf_max, ft_surf_min, ft_sub_max, ft_sub_min;
     int packed;
     double2 *s_np, *s_tl, *s_fu, *cs_cur;                     // packed RHS records (when packed)
+    int *sfl;                                                 // packed seg_first words: bit 31 = LAI > ZERO
 };
 
 void launch_et_kernel(const DevEt &e, const EtStepDev &s, DevErr *err, hipStream_t st);

@@ -120,7 +120,15 @@ struct shud_out {
     std::deque<OutTask> tasks[kWriters];
     int bank_left[2] = {0, 0};           // rows of the bank's event not yet written
     bool stop = false;
+    // first writer-side failure (the snapshot copy's event or a file write): reported by shud_out_flush /
+    // shud_out_rows / shud_out_destroy; rows whose copy failed are never written (no stale bank reaches a file)
+    int werr = 0;
+    std::string werr_msg;
 };
+static void writer_fail(shud_out *o, int code, const std::string &msg) {
+    std::lock_guard<std::mutex> lk(o->mu);
+    if (!o->werr) { o->werr = code; o->werr_msg = msg; }
+}
 
 static void writer_loop(shud_out *o, int w) {
     (void)hipSetDevice(o->device);
@@ -133,17 +141,24 @@ static void writer_loop(shud_out *o, int w) {
             job = o->tasks[w].front();
             o->tasks[w].pop_front();
         }
-        (void)hipEventSynchronize(o->ev_copied[job.bank]);
+        const hipError_t he = hipEventSynchronize(o->ev_copied[job.bank]);
         PrintCtrl &p = o->pc[job.ctrl];
         const double *hb = p.h_buf[job.bank];
-        if (p.fa) {                                                  // fun_printASCII
-            fprintf(p.fa, "%.1f\t", job.tq);
-            for (int i = 0; i < p.numvar; i++) fprintf(p.fa, "%e\t", hb[i]);
-            fprintf(p.fa, "\n");
-        }
-        if (p.fb) {                                                  // fun_printBINARY
-            fwrite(&job.tq, sizeof(double), 1, p.fb);
-            fwrite(hb, sizeof(double), p.numvar, p.fb);
+        if (he != hipSuccess) {
+            writer_fail(o, SHUD_ERR_HIP, std::string("output snapshot copy failed (") + hipGetErrorString(he) +
+                                             "): row of " + p.filename + " not written");
+        } else {
+            if (p.fa) {                                              // fun_printASCII
+                fprintf(p.fa, "%.1f\t", job.tq);
+                for (int i = 0; i < p.numvar; i++) fprintf(p.fa, "%e\t", hb[i]);
+                fprintf(p.fa, "\n");
+                if (ferror(p.fa)) writer_fail(o, SHUD_ERR_ARG, "write error on " + p.filename + ".csv");
+            }
+            if (p.fb) {                                              // fun_printBINARY
+                const size_t w1 = fwrite(&job.tq, sizeof(double), 1, p.fb);
+                const size_t w2 = fwrite(hb, sizeof(double), p.numvar, p.fb);
+                if (w1 != 1 || w2 != (size_t)p.numvar) writer_fail(o, SHUD_ERR_ARG, "write error on " + p.filename + ".dat");
+            }
         }
         {
             std::lock_guard<std::mutex> lk(o->mu);
@@ -153,14 +168,18 @@ static void writer_loop(shud_out *o, int w) {
     }
 }
 
-// wait until every queued row is in the files (flushed to the C library)
-static void out_drain(shud_out *o) {
+// wait until every queued row is in the files (flushed to the C library); returns the first writer failure
+static int out_drain(shud_out *o) {
     std::unique_lock<std::mutex> lk(o->mu);
     o->cv.wait(lk, [&] { return o->bank_left[0] == 0 && o->bank_left[1] == 0; });
     for (PrintCtrl &p : o->pc) {
-        if (p.fb) fflush(p.fb);
-        if (p.fa) fflush(p.fa);
+        if (p.fb && fflush(p.fb) != 0 && !o->werr) { o->werr = SHUD_ERR_ARG; o->werr_msg = "flush error on " + p.filename + ".dat"; }
+        if (p.fa && fflush(p.fa) != 0 && !o->werr) { o->werr = SHUD_ERR_ARG; o->werr_msg = "flush error on " + p.filename + ".csv"; }
     }
+    return o->werr;
+}
+static int out_report(shud_out *o) {
+    return o->werr ? shud_fail(o->werr, "shud_out: %s", o->werr_msg.c_str()) : SHUD_OK;
 }
 
 static int out_fail_io(const char *what, const std::string &f) {
@@ -189,7 +208,7 @@ extern "C" int shud_out_add(shud_out_t o, const ShudPrintSpec *s) {
                                            s->basename);
     if (s->n_all < 0 || s->interval < 0) return shud_fail(SHUD_ERR_ARG, "bad n_all / interval");
     HIP_TRY(hipSetDevice(o->device));
-    out_drain(o);                        // the writer indexes pc: no rows in flight while it grows
+    if (out_drain(o)) return out_report(o);   // the writer indexes pc: no rows in flight while it grows
     PrintCtrl p;
     p.filename = s->basename;
     p.start_time = (long long)s->start_time;
@@ -291,7 +310,6 @@ extern "C" int shud_out_export(shud_out_t o, double t) {
         std::unique_lock<std::mutex> lk(o->mu);
         o->cv.wait(lk, [&] { return o->bank_left[bank] == 0; });
     }
-    o->bank ^= 1;
     // the snapshots are free once the previous copy has finished
     if (o->copy_pending) HIP_TRY(hipStreamWaitEvent(o->stream, o->ev_copied[bank ^ 1], 0));
     for (const auto &r : rows) {
@@ -300,8 +318,6 @@ extern "C" int shud_out_export(shud_out_t o, double t) {
         if (p.numvar > 0)
             hipLaunchKernelGGL(k_snap, dim3((p.numvar + 255) / 256), dim3(256), 0, o->stream, p.d_buf, p.d_snap,
                                p.numvar, f);
-        p.num_update = 0;
-        p.rows++;
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(o->ev_snap, o->stream));
@@ -313,6 +329,14 @@ extern "C" int shud_out_export(shud_out_t o, double t) {
                                    o->s_copy));
     }
     HIP_TRY(hipEventRecord(o->ev_copied[bank], o->s_copy));
+    // every launch and copy is enqueued: only now are the rows committed (a failure above returns with the
+    // intervals still open and nothing queued for the writers)
+    for (const auto &r : rows) {
+        PrintCtrl &p = o->pc[r.ctrl];
+        p.num_update = 0;
+        p.rows++;
+    }
+    o->bank ^= 1;
     o->copy_pending = true;
     {
         std::lock_guard<std::mutex> lk(o->mu);
@@ -326,12 +350,12 @@ extern "C" int shud_out_export(shud_out_t o, double t) {
 extern "C" int shud_out_flush(shud_out_t o) {
     if (!o) return shud_fail(SHUD_ERR_ARG, "null argument");
     out_drain(o);
-    return SHUD_OK;
+    return out_report(o);
 }
 
 extern "C" int64_t shud_out_rows(shud_out_t o, int k) {
     if (!o || k < 0 || k >= (int)o->pc.size()) return -1;
-    out_drain(o);
+    if (out_drain(o)) return out_report(o);          // a writer failure: its (negative) error code
     return o->pc[k].rows;
 }
 
@@ -339,6 +363,7 @@ extern "C" int shud_out_destroy(shud_out_t o) {
     if (!o) return SHUD_OK;
     (void)hipSetDevice(o->device);
     out_drain(o);
+    const int rc = out_report(o);
     {
         std::lock_guard<std::mutex> lk(o->mu);
         o->stop = true;
@@ -363,7 +388,7 @@ extern "C" int shud_out_destroy(shud_out_t o) {
         if (o->ev_copied[b]) (void)hipEventDestroy(o->ev_copied[b]);
     if (o->s_copy) (void)hipStreamDestroy(o->s_copy);
     delete o;
-    return SHUD_OK;
+    return rc;
 }
 
 // ---------------------------------------------------------------------------------------------

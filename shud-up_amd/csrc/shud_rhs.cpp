@@ -508,49 +508,37 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         h->rseg_perm = rorder;
     }
     std::vector<double2> rv(4 * (size_t)NR);
+    std::vector<int4> ri(NR), ru(NR);
     const int nor = h->n_own_riv;
-    std::vector<int4> ri(nor);
-    std::vector<double2> rdn(2 * (size_t)nor), upr(4 * (size_t)up_off[nor]);
-    auto pack_ib = [](int a, int b) {                        // two int32 in one double slot
-        double v;
-        const int32_t two[2] = {a, b};
-        memcpy(&v, two, sizeof v);
-        return v;
-    };
-    auto down_of = [&](int r) { return (h->lakeon && m->riv_down[r] <= -4) ? -3 : m->riv_down[r]; };  // lake: outlet
-    auto bc_of = [&](int r) { return m->riv_bc ? m->riv_bc[r] : 0; };
     for (int r = 0; r < NR; r++) {
+        const int dn = (h->lakeon && m->riv_down[r] <= -4) ? -3 : m->riv_down[r];   // into a lake: outlet formula
+        const int bc = m->riv_bc ? m->riv_bc[r] : 0;
+        double ib;                                                   // (down, BC) packed into the 4th slot
+        const int32_t two[2] = {dn, bc};
+        memcpy(&ib, two, sizeof ib);
         rv[4 * (size_t)r + 0] = make_double2(m->riv_bottom_width[r], m->riv_bankslope[r]);
         rv[4 * (size_t)r + 1] = make_double2(m->riv_length[r], m->riv_bed_slope[r]);
         rv[4 * (size_t)r + 2] = make_double2(m->riv_dist2down[r], m->riv_avg_rough[r]);
-        rv[4 * (size_t)r + 3] = make_double2(m->riv_depth[r], pack_ib(down_of(r), bc_of(r)));
-    }
-    // owned reaches: segment range, upstream CSR, and the downstream / upstream QrivDown statics (same
-    // expressions and order as the kernel computed them: smean = (slope + slope_down) * 0.5; -ffp-contract=off)
-    for (int r = 0; r < nor; r++) {
-        ri[r] = make_int4(rstart[r], rcnt[r], up_off[r], up_off[r + 1] - up_off[r]);
-        const int dn = down_of(r);
-        const int d = dn >= 0 ? dn : r;                      // outlets: harmless self load
-        if (dn >= 0 && !cdiv_divisor_ok(m->riv_dist2down[r])) return 0;
-        rdn[2 * (size_t)r] = make_double2(dn >= 0 ? (m->riv_bed_slope[r] + m->riv_bed_slope[d]) * 0.5 : 0.,
-                                          dn >= 0 ? m->riv_depth[d] : 0.);
-        rdn[2 * (size_t)r + 1] = make_double2(dn >= 0 ? 1. / m->riv_dist2down[r] : 0., pack_ib(d, bc_of(d)));
-        for (int k = up_off[r]; k < up_off[r + 1]; k++) {
-            const int u = up_idx[k];
-            if (!cdiv_divisor_ok(m->riv_dist2down[u])) return 0;
-            upr[4 * (size_t)k + 0] = make_double2(m->riv_bottom_width[u], m->riv_bankslope[u]);
-            upr[4 * (size_t)k + 1] = make_double2(m->riv_depth[u], m->riv_dist2down[u]);
-            upr[4 * (size_t)k + 2] = make_double2(m->riv_avg_rough[u], (m->riv_bed_slope[u] + m->riv_bed_slope[r]) * 0.5);
-            upr[4 * (size_t)k + 3] = make_double2(pack_ib(u, bc_of(u)), 1. / m->riv_dist2down[u]);
+        rv[4 * (size_t)r + 3] = make_double2(m->riv_depth[r], ib);
+        ri[r] = make_int4(dn, bc, rstart[r], rcnt[r]);
+        int4 u = make_int4(0, 0, 0, 0);
+        if (r < nor) {
+            const int n = up_off[r + 1] - up_off[r];
+            if (n <= 3) {
+                int v[3] = {0, 0, 0};
+                for (int k = 0; k < n; k++) v[k] = up_idx[up_off[r] + k];
+                u = make_int4(v[0], v[1], v[2], n);
+            } else {
+                u = make_int4(0, 0, 0, -1);
+            }
         }
+        ru[r] = u;
     }
-    double2 *rv_d, *rdn_d, *upr_d; int4 *ri_d;
+    double2 *rv_d; int4 *ri_d, *ru_d;
     if ((rc = h->upload(&rv_d, rv.data(), rv.size()))) return rc;
-    // (at least one entry each, zero-filled when empty, so the device pointers are never null)
-    if ((rc = h->upload(&ri_d, ri.empty() ? nullptr : ri.data(), std::max<size_t>(ri.size(), 1)))) return rc;
-    if ((rc = h->upload(&rdn_d, rdn.empty() ? nullptr : rdn.data(), std::max<size_t>(rdn.size(), 1)))) return rc;
-    if ((rc = h->upload(&upr_d, upr.empty() ? nullptr : upr.data(), std::max<size_t>(upr.size(), 1)))) return rc;
-    P.rv = rv_d; P.rv_i = ri_d; P.rv_dn = rdn_d; P.upr = upr_d;
+    if ((rc = h->upload(&ri_d, ri.data(), NR))) return rc;
+    if ((rc = h->upload(&ru_d, ru.data(), NR))) return rc;
+    P.rv = rv_d; P.rv_i = ri_d; P.rv_u = ru_d;
     h->n_classes = ncls;
     h->packed = true;
     return 0;
@@ -752,7 +740,7 @@ extern "C" int shud_rhs_set_step_inputs(shud_rhs_t h, const ShudStepInputs *in) 
         if (in->fu_sub) h->fu_unit[1] = all_ones(in->fu_sub);
         unsigned what = 0;
         if (in->net_prep || in->pot_evap) what |= 1;
-        if (in->pot_tran || in->lai) what |= 2;
+        if (in->pot_tran || in->lai || in->etp) what |= 2;
         if (in->fu_surf || in->fu_sub) what |= 4;
         if (in->u_satn) what |= 8;
         if (in->e_ic) what |= 16;

@@ -338,9 +338,11 @@ class Output:
         _check(lib().shud_out_flush(self.h), "shud_out_flush")
 
     def close(self):
+        """shud_out_destroy; raises if the asynchronous writer failed (a lost row or a file write error)"""
         if self.h:
-            lib().shud_out_destroy(self.h)
+            rc = lib().shud_out_destroy(self.h)
             self.h = None
+            _check(rc, "shud_out_destroy")
 
     def __del__(self):
         try:

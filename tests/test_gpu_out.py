@@ -145,3 +145,32 @@ def test_solver_loop_exports_on_device(tmp_path):
         assert open(tmp_path / f"dev{k}.dat", "rb").read() == open(tmp_path / f"ref{k}.dat", "rb").read(), k
     sv.close()
     h.close()
+
+
+def test_writer_errors_surface(tmp_path):
+    """A failing output file (the .dat opened on /dev/full: every write or flush fails with ENOSPC) is
+    reported by shud_out_flush and shud_out_destroy instead of being dropped silently; a healthy
+    control beside it keeps its rows."""
+    m, y0 = cases.ccw()
+    m.step = workload.random_step_inputs(m, seed=3)
+    h = rt.RhsHandle(m)
+    h.set_step_inputs()
+    dy, ddy = h.device_alloc(8 * m.num_y), h.device_alloc(8 * m.num_y)
+    h.h2d(dy, y0)
+    h.eval_device(0.0, dy, ddy)
+    h.summary(dy)
+    p, n = h.device_array(abi.SHUD_ARR_Y_ELE_SURF)
+    (tmp_path / "full.dat").symlink_to("/dev/full")
+    out = rt.Output(stream=h.stream())
+    out.add(tmp_path / "ok", p, n, 30, 0)
+    out.add(tmp_path / "full", p, n, 30, 0)
+    for t in (30.0, 60.0, 90.0):
+        out.export(t)
+    with pytest.raises(rt.ShudRhsError):
+        out.flush()
+    with pytest.raises(rt.ShudRhsError):
+        out.close()
+    assert read_dat(tmp_path / "ok.dat")["data"].shape == (3, n)
+    h.device_free(dy)
+    h.device_free(ddy)
+    h.close()
