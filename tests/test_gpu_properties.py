@@ -68,8 +68,9 @@ def test_run_to_run_determinism(n, seed, mode):
 
 
 # the CPU restatement integrates sequentially: sizes just past the 2048-block reduction grid exercise the
-# grid-stride tail without spending minutes in the oracle (12 examples up to 2600 blocks took 133 s)
-@settings(max_examples=8, deadline=None, derandomize=True,
+# grid-stride tail without spending minutes in the oracle (12 examples up to 2600 blocks took 133 s, 8 up to 2100
+# blocks 83 s; 5 keep both size bands under derandomize)
+@settings(max_examples=5, deadline=None, derandomize=True,
           suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
 @given(blocks=st.one_of(st.integers(0, 300), st.integers(2044, 2100)), tail=st.integers(1, 255),
        rtol_e=st.integers(4, 8), atol_e=st.integers(8, 12), h0_e=st.integers(2, 6))
