@@ -184,7 +184,10 @@ def main():
     ms_eval = ms_eval_loop
     if world > 1 and args.profile_reps > 0:
         _, per_ser = h.time_kernels(0.0, yp, dyp, args.profile_reps)
-        per["halo_exchange_serialized"] = per_ser.get("halo_exchange")
+        # pack + grouped send/recv alone (serialized, no overlap), slowest rank
+        th = torch.tensor([float(per_ser.get("halo_exchange") or 0.0)], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(th, op=dist.ReduceOp.MAX)
+        per["halo_exchange_serialized"] = float(th.item())
         dist.barrier()
     ms_ele = per["shud_ele_kernel"]
     ms_riv = per["shud_riv_kernel"]
