@@ -152,13 +152,18 @@ static void v_linear_sum(long n, double a, const double *x, double b, const doub
 }
 
 /* Reduction order.  0: the serial N_Vector's (one left-to-right sum, nvector_serial.c) — CVODE's own order.
- * 1: the device integrator's fixed order (shud-up_amd/csrc/shud_ode_kernels.hip): a grid of
- * B = min(ceil(n/256), ORACLE_RED_BLOCKS) blocks x 256 threads; thread (b, t) sums entries b*256 + t + k*256*B in k order from
- * 0.0; each 64-lane wave combines by an xor butterfly (offsets 32..1, own value first) and lane 0 keeps the
- * result; the block adds its 4 wave results in wave order; a one-block pass then does the same over the B
- * block partials.  With order 1 the restatement reproduces the device integrator bit for bit wherever the RHS
- * is IEEE-exact (tests/test_gpu_ode.py). */
-#define ORACLE_RED_BLOCKS 2048   /* shud_ode_dev.h kMaxBlocks (8192 measured: no faster reductions, finalize 6 -> 17 us) */
+ * 1: the device integrator's fixed order (shud-up_amd/csrc/shud_ode_kernels.hip, round 3): one entry per thread on
+ * a grid of B = ceil(n/1024) blocks x 1024 threads; thread (b, t) holds 0.0 + term[b*1024 + t] (0.0 past n); each
+ * 64-lane wave combines by an xor butterfly (offsets 32..1, own value first) and lane 0 keeps the result; the block
+ * combines its 16 wave results by an xor butterfly over offsets 8..1 (lane 0) into partial[b].  The one-block finalize (1024 threads): thread t keeps 4
+ * accumulators from 0.0, acc[k] += partial[t + (4j + k)*1024] for j = 0, 1, ... (0.0 past B); x = (acc0 + acc1) +
+ * (acc2 + acc3); wave butterfly; the 16 wave results by the 16-lane butterfly.  With order 1 the restatement reproduces the
+ * device integrator bit for bit wherever the RHS is IEEE-exact (tests/test_gpu_ode.py).  (Round 2's order — a
+ * 2048-block grid-stride loop of 256-thread blocks — ran the five-operand passes at 4.7 TB/s against 5.7 TB/s
+ * one-shot: profiles/r03/ode/.) */
+#define ORACLE_RED_THREADS 1024   /* shud_ode_dev.h kRedThreads */
+#define ORACLE_FIN_THREADS 1024   /* kFinThreads */
+#define ORACLE_FIN_ACC 4          /* kFinAcc */
 static int g_red_order = 0;
 void oracle_ode_set_reduction_order(int order) { g_red_order = order; }
 
@@ -171,32 +176,44 @@ static double wave_butterfly(double *x) {        /* x[64], destroyed; returns la
     return x[0];
 }
 
-static double block_combine(double *lanes) {     /* lanes[256] -> 4 wave results in wave order */
-    double s = wave_butterfly(lanes);
-    for (int w = 1; w < 4; ++w) s = s + wave_butterfly(lanes + 64 * w);
-    return s;
+/* lanes[nthreads] -> each wave's butterfly result, then those nw = nthreads/64 results by an xor butterfly over
+ * offsets nw/2 .. 1 (kernel waves_tree), lane 0 */
+static double waves_in_order(double *lanes, int nthreads) {
+    const int nw = nthreads / 64;
+    double w[64], y[64];
+    for (int k = 0; k < nw; ++k) w[k] = wave_butterfly(lanes + 64 * k);
+    for (int off = nw / 2; off >= 1; off >>= 1) {
+        for (int l = 0; l < nw; ++l) y[l] = w[l] + w[l ^ off];
+        memcpy(w, y, nw * sizeof(double));
+    }
+    return w[0];
 }
 
 static double device_order_sum(long n, const double *term) {
-    long nb = (n + 255) / 256;
+    long nb = (n + ORACLE_RED_THREADS - 1) / ORACLE_RED_THREADS;
     if (nb < 1) nb = 1;
-    if (nb > ORACLE_RED_BLOCKS) nb = ORACLE_RED_BLOCKS;
-    static double part[ORACLE_RED_BLOCKS];
-    double lanes[256];
+    static double *part = NULL;
+    static long part_n = 0;
+    if (nb > part_n) { free(part); part = (double *)malloc(nb * sizeof(double)); part_n = nb; }
+    double lanes[ORACLE_RED_THREADS > ORACLE_FIN_THREADS ? ORACLE_RED_THREADS : ORACLE_FIN_THREADS];
     for (long b = 0; b < nb; ++b) {
-        for (int t = 0; t < 256; ++t) {
-            double acc = 0.0;
-            for (long i = b * 256 + t; i < n; i += 256 * nb) acc += term[i];
-            lanes[t] = acc;
+        for (int t = 0; t < ORACLE_RED_THREADS; ++t) {
+            const long i = b * ORACLE_RED_THREADS + t;
+            lanes[t] = i < n ? 0.0 + term[i] : 0.0;
         }
-        part[b] = block_combine(lanes);
+        part[b] = waves_in_order(lanes, ORACLE_RED_THREADS);
     }
-    for (int t = 0; t < 256; ++t) {
-        double acc = 0.0;
-        for (long b = t; b < nb; b += 256) acc = acc + part[b];
-        lanes[t] = acc;
+    for (int t = 0; t < ORACLE_FIN_THREADS; ++t) {
+        double acc[ORACLE_FIN_ACC];
+        for (int k = 0; k < ORACLE_FIN_ACC; ++k) acc[k] = 0.0;
+        for (long b0 = t; b0 < nb; b0 += (long)ORACLE_FIN_ACC * ORACLE_FIN_THREADS)
+            for (int k = 0; k < ORACLE_FIN_ACC; ++k) {
+                const long b = b0 + (long)k * ORACLE_FIN_THREADS;
+                acc[k] = acc[k] + (b < nb ? part[b] : 0.0);
+            }
+        lanes[t] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
     }
-    return block_combine(lanes);
+    return waves_in_order(lanes, ORACLE_FIN_THREADS);
 }
 
 static double *g_term = NULL;

@@ -73,6 +73,10 @@ struct shud_ode {
     // device vectors
     double *base = nullptr, *zn = nullptr, *ewt = nullptr, *y = nullptr, *acor = nullptr, *ftemp = nullptr;
     double *tempv = nullptr, *delta = nullptr, *work = nullptr, *V = nullptr;
+    // the next step's error weights, computed by the fused complete+ewt pass; swapped in by ewt_and_norm
+    double *ewt_alt = nullptr;
+    bool ewt_pending = false;
+    int64_t ewt_fin_sync = 0;           // n_sync when the fused pass's finalize was enqueued
     double *d_part = nullptr, *d_ds = nullptr, *h_ds = nullptr;
     Red red{};
     Red rs(int slot) const { Red r = red; r.slot0 = slot; return r; }   // this reduction's result slots
@@ -179,14 +183,19 @@ struct shud_ode {
         gamrat = (nst > 0) ? gamma / gammap : 1.0;
     }
     // ---- cvPredict / cvRestore / cvRescale ----
+    // y_pred: the last predict also wrote y = zn[0] + 0 and acor = 0 (k_pascal), which the cvNls start that
+    // always follows it would otherwise do in a separate pass (k_vsum_zero)
+    bool y_pred = false;
     void predict() {
         tn += h;
         if (tstopset && (tn - tstop) * h > 0.0) tn = tstop;
-        ode::predict(n, zn, q, s);
+        ode::predict(n, zn, q, y, acor, s);
+        y_pred = true;
     }
     void restore(double saved_t) {
         tn = saved_t;
         ode::restore(n, zn, q, s);
+        y_pred = false;
     }
     void rescale() {
         Coefs c{};
@@ -380,8 +389,9 @@ struct shud_ode {
         // the residual reads no ycor (identical operands, one fewer pass over HBM)
         const bool az = acor_zero;
         acor_zero = false;
-        if (az) vsum_zero(n, Z(0), acor, y, s);
-        else vsum(n, Z(0), acor, y, s);
+        if (az && !y_pred) vsum_zero(n, Z(0), acor, y, s);
+        else if (!az) vsum(n, Z(0), acor, y, s);
+        y_pred = false;
         if (rhs(tn, y, ftemp) != 0) return SHUD_ODE_RHSFUNC_FAIL;
         nfe++;
         residual(n, Z(1), az ? nullptr : acor, ftemp, rl1, -gamma, ewt, delta, rs(S_RES), s);
@@ -524,7 +534,11 @@ struct shud_ode {
             saved_tq5 = tq[5];
             indx_acor = qmax;
         }
-        complete_step(n, zn, acor, lc, q, copy_to, s);
+        // cvCompleteStep + the next loop iteration's cvEwtSet / N_VWrmsNorm(zn[0]) in one pass (ewt_and_norm)
+        complete_step_ewt(n, zn, acor, lc, q, copy_to, rtol, atol, ewt_alt, rs(S_EWTMIN), s);
+        finalize(rs(S_EWTMIN), 2, 1u, s);
+        ewt_pending = true;
+        ewt_fin_sync = n_sync;
         // cvPrepareNextStep
         if (etamax == 1.0) {
             qwait = qwait > 2 ? qwait : 2;
@@ -621,6 +635,12 @@ struct shud_ode {
         return SHUD_ODE_SUCCESS;
     }
     int ewt_and_norm() {                                              // cvEwtSet + N_VWrmsNorm(zn[0])
+        if (ewt_pending) {              // computed by the last complete_step_ewt on this zn[0]
+            std::swap(ewt, ewt_alt);
+            ewt_pending = false;
+            if (n_sync == ewt_fin_sync && !fetch()) return -1;          // no synchronize since its finalize
+            return h_ds[S_EWTMIN] <= 0.0 ? 1 : 0;
+        }
         ewt_set(n, Z(0), ewt, rtol, atol, rs(S_EWTMIN), s);
         finalize(rs(S_EWTMIN), 2, 1u, s);
         if (!fetch()) return -1;
@@ -758,7 +778,7 @@ static int ode_alloc(shud_ode *o, double t0, const double *y0, int where, const 
     o->tn = t0;
     o->nrmfac = std::sqrt((double)o->n);
     const int64_t n = o->n;
-    const int64_t nvec = (o->qmax + 1) + 7 + (o->maxl + 1);
+    const int64_t nvec = (o->qmax + 1) + 8 + (o->maxl + 1);
     HIP_TRY(hipMalloc(&o->base, nvec * n * sizeof(double)));
     double *p = o->base;
     o->zn = p; p += (int64_t)(o->qmax + 1) * n;
@@ -769,9 +789,10 @@ static int ode_alloc(shud_ode *o, double t0, const double *y0, int where, const 
     o->tempv = p; p += n;
     o->delta = p; p += n;
     o->work = p; p += n;
+    o->ewt_alt = p; p += n;
     o->V = p;
     HIP_TRY(hipMemsetAsync(o->base, 0, nvec * n * sizeof(double), o->s));
-    HIP_TRY(hipMalloc(&o->d_part, (size_t)kMaxAcc * kMaxBlocks * sizeof(double)));
+    HIP_TRY(hipMalloc(&o->d_part, (size_t)kMaxAcc * grid_blocks(n) * sizeof(double)));
     HIP_TRY(hipMalloc(&o->d_ds, S_COUNT * sizeof(double)));
     HIP_TRY(hipMemsetAsync(o->d_ds, 0, S_COUNT * sizeof(double), o->s));
     HIP_TRY(hipHostMalloc(&o->h_ds, (S_COUNT + 1) * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent));

@@ -4,8 +4,9 @@
 // Every kernel is one streaming pass over NY-long fp64 vectors in HBM, fusing the N_Vector operations that
 // CVODE issues back to back (cvode.c / sunlinsol_spgmr.c / nvector_serial.c) so each pass reads every operand
 // once.  Per element the arithmetic is exactly the serial N_Vector kernel's (same operations, same order, no
-// FMA contraction: -ffp-contract=off).  Reductions (dot products, WRMS norms, min) are deterministic: a fixed
-// grid writes per-block partials in a fixed order, and a one-block finalize kernel sums them in a fixed order
+// FMA contraction: -ffp-contract=off).  Reductions (dot products, WRMS norms, min) are deterministic: one entry
+// per thread on a full grid of kRedThreads-thread blocks writes per-block partials (waves in order), and a
+// one-block finalize kernel (kFinThreads threads, kFinAcc interleaved accumulators each) sums them in a fixed order
 // into a device scalar slot `ds[slot]` that later kernels read directly, and into its host-mapped twin
 // `hds[slot]` (with the RHS error word) that the host reads after a stream synchronize — no copy per fetch.
 #pragma once
@@ -16,8 +17,10 @@
 namespace shud {
 namespace ode {
 
-constexpr int kThreads = 256;
-constexpr int kMaxBlocks = 2048;
+constexpr int kThreads = 256;       // element-wise passes
+constexpr int kRedThreads = 1024;   // reduction passes: one entry per thread, ceil(n / 1024) blocks
+constexpr int kFinThreads = 1024;   // finalize: thread t sums partials t + (kFinAcc*j + k)*kFinThreads into acc k
+constexpr int kFinAcc = 4;
 constexpr int kMaxAcc = 4;
 constexpr int kMaxL = 32;     // SPGMR Krylov dimension bound (maxl)
 constexpr int kQMax = 5;      // BDF
@@ -41,8 +44,8 @@ enum Slot : int {
 };
 
 struct Red {           // partial-sum scratch of one reduction launch and where its result goes
-    double *part;      // [kMaxAcc][kMaxBlocks]
-    int nblk;          // blocks of the producing grid (fixed per n)
+    double *part;      // [kMaxAcc][nblk]
+    int nblk;          // blocks of the producing grid, ceil(n / kRedThreads) (fixed per n); also the stride of part
     double *ds;        // device scalar slots [S_COUNT]
     double *hds;       // host-mapped twin [S_COUNT + 1]; hds[S_COUNT] carries the RHS error word
     const uint32_t *err;   // RHS error flags (DevErr::flags) or null
@@ -58,7 +61,8 @@ struct Coefs {         // small host-computed coefficient arrays passed by value
 void finalize(const Red &r, int nacc, unsigned minmask, hipStream_t s);
 
 void ewt_set(int64_t n, const double *zn0, double *ewt, double rtol, double atol, const Red &r, hipStream_t s);
-void predict(int64_t n, double *zn, int q, hipStream_t s);
+// cvPredict; with y/ycor != null also ycor = 0 and y = zn[0] + 0.0 (the following cvNls start)
+void predict(int64_t n, double *zn, int q, double *y, double *ycor, hipStream_t s);
 void restore(int64_t n, double *zn, int q, hipStream_t s);
 void rescale(int64_t n, double *zn, int q, const Coefs &c, hipStream_t s);
 void vsum(int64_t n, const double *x, const double *y, double *z, hipStream_t s);
@@ -90,6 +94,9 @@ void newton_update(int64_t n, const double *V, int64_t vstride, int krydim, cons
                    const double *ewt, double *ycor, const Red &r, hipStream_t s);
 // zn[j] = l[j]*acor + zn[j], j = 0..q; if copy_to >= 0: zn[copy_to] = acor
 void complete_step(int64_t n, double *zn, const double *acor, const Coefs &l, int q, int copy_to, hipStream_t s);
+// complete_step, then ewt_set's arithmetic on the new zn[0] into ewt_next; r: [min(rtol|y| + atol), sum (y*w)^2]
+void complete_step_ewt(int64_t n, double *zn, const double *acor, const Coefs &l, int q, int copy_to, double rtol,
+                       double atol, double *ewt_next, const Red &r, hipStream_t s);
 // r: [sum (zn_q*ewt)^2 (zn_q != NULL), sum (((-cquot)*zn_qmax + acor)*ewt)^2 (zn_qmax != NULL)]
 void eta_norms(int64_t n, const double *zn_q, const double *zn_qmax, const double *acor, double ncquot,
                const double *ewt, const Red &r, hipStream_t s);

@@ -6,11 +6,12 @@
 #   bench        the driver's command: bench.py --gpus 1 --steps 20 --warmup 5
 #   quick        RHS-only bench line (no CPU baseline / ET / integrator / e2e)
 #   ab:L1,L2     tools/ab_variants.py on the production lib and each build/ab/libshud_rhs_<L>.so
+#   odeab:L1,L2  integrator ms/step (bench.py integrator section) for the production lib and each A/B lib, twice
 #   kt           rocprofv3 kernel trace of the RHS-only bench            pmc   FETCH_SIZE / WRITE_SIZE passes -> summary
 #   sq           SQ / GRBM counter passes (tools/sq_counters.sh)          ode   integrator kernel trace
 #   part1        bench's N>1 code path on one rank                        rank  tools/rank_timing.py (2/4/8-way)
 #   e2e          tools/profile_e2e.sh 1M, 1 day                          redbench  tools/ode_red_bench (reduction forms)
-#   test:EXPR    pytest -m gpu -k EXPR
+#   test:EXPR    pytest -m gpu -k EXPR                                    traj  tests/diag_traj_day.py (ccw one day)
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=$1; shift
@@ -31,6 +32,16 @@ for step in "$@"; do
         SHUD_RHS_LIB=$PWD/shud-up_amd/build/ab/libshud_rhs_$n.so timeout -k 10 300 python tools/ab_variants.py --variants pk --rounds 5 > "$O/ab_$n.log" 2>&1
       done
       for f in prod ${libs//,/ }; do echo "$f $(tail -n 1 "$O/ab_$f.log")"; done > "$O/ab_summary.log" ;;
+    odeab:*)
+      libs="${step#odeab:}"
+      B="--no-cpu-baseline --no-et --no-many-class --no-host-vectors --e2e-ele 0 --steps 5 --warmup 1"
+      for rep in 1 2; do
+        for n in prod ${libs//,/ }; do
+          if [ $n = prod ]; then L=""; else L=$PWD/shud-up_amd/build/ab/libshud_rhs_$n.so; fi
+          SHUD_RHS_LIB=$L timeout -k 10 300 python bench.py $B > "$O/odeab_${n}_$rep.json" 2> "$O/odeab_${n}_$rep.err"
+          echo "$n rep$rep $(python -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['integrator']['ms_per_step'], d['integrator']['steps'])" "$O/odeab_${n}_$rep.json")" >> "$O/odeab_summary.log"
+        done
+      done ;;
     kt) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt" -o run -- python3 bench.py $A --steps 20 --warmup 5 > "$O/bench_kt.json" 2> "$O/bench_kt.err" ;;
     pmc)
       timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch" -o run -- python3 bench.py $A --steps 5 --warmup 1 > "$O/pmc_fetch.log" 2>&1
@@ -41,6 +52,7 @@ for step in "$@"; do
     part1) timeout -k 10 300 python bench.py $A --partition-1 --steps 20 > "$O/bench_partition1.json" 2> "$O/bench_partition1.err" ;;
     rank) timeout -k 10 400 python tools/rank_timing.py > "$O/rank_timing.json" 2> "$O/rank_timing.err" ;;
     e2e) timeout -k 10 600 bash tools/profile_e2e.sh 1000000 1 > "$O/e2e.log" 2>&1 ;;
+    traj) timeout -k 10 300 python tests/diag_traj_day.py "$O/traj_ccw_day.json" > "$O/traj_ccw_day.log" 2>&1 ;;
     redbench) timeout -k 10 120 tools/ode_red_bench 31000000 30 > "$O/ode_red_bench.log" 2>&1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

@@ -21,6 +21,7 @@ PER_ENTRY = {
     "k_normalize": lambda q: 24,
     "k_newton_update": lambda q: 8 * (3 + 2),   # ewt, ycor, ~2 Krylov vectors, ycor
     "k_complete": lambda q: 8 * (1 + 2 * (q + 1)),
+    "k_complete_ewt": lambda q: 8 * (1 + 2 * (q + 1)) + 8,   # + the next step's ewt (round 3)
     "k_rescale": lambda q: 16 * q,
     "k_eta_norms": lambda q: 32,
 }
@@ -40,9 +41,11 @@ def main():
         name = r["Name"]
         m = re.search(r"(k_\w+?)(?:<|\(|I)", name.replace("shud::ode::", ""))
         if "pascal" in name:
-            q = int(re.search(r"k_pascal<(\d)", name).group(1))
-            b = 8 * (2 * q + 1)
-            key = f"k_pascal<{q}>"
+            mm = re.search(r"k_pascal<(\d), (true|false)", name)
+            q = int(mm.group(1))
+            fwd = mm.group(2) == "true"
+            b = 8 * (2 * q + 1) + (16 if fwd else 0)      # predict also writes y and ycor (round 3)
+            key = f"k_pascal<{q},{'pred' if fwd else 'rest'}>"
         elif m and m.group(1) in PER_ENTRY:
             key = m.group(1)
             b = PER_ENTRY[key](a.q)
