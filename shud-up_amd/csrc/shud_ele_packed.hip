@@ -18,8 +18,6 @@
 #include <stdint.h>
 #include <stdlib.h>
 
-#include <algorithm>
-
 #include "shud_dev.h"
 #include "shud_physics.h"
 
@@ -95,11 +93,9 @@ constexpr int CF_LDS_STRIDE = CF_STRIDE;   // the HBM table's record layout, cop
 #ifndef SHUD_ELE_WAVES
 #define SHUD_ELE_WAVES 5        // min waves per SIMD: <= 96 VGPRs (rolled edge loop, no spills)
 #endif
-// SHUD_ELE_PERSIST: 1 = persistent workgroups (one per resident slot, each looping over XCD-chunked 256-element
-// tiles; the class table is copied to LDS once per workgroup instead of once per tile), 0 = one tile per workgroup
-#ifndef SHUD_ELE_PERSIST
-#define SHUD_ELE_PERSIST 0
-#endif
+// One 256-element tile per workgroup.  (Persistent workgroups — one per resident slot looping over XCD-chunked
+// tiles, the class table copied to LDS once per workgroup — measured 0.735 vs 0.657 ms: the tile loop took the
+// kernel to 96 VGPRs with spills, profiles/r03/ab_persist/.)
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
 __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, const YView &Y, double *__restrict__ dy,
                                          int i, int cur, const DevDiag &dg, const DevLake &lk, const double *lct);
@@ -114,19 +110,8 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         for (int t = threadIdx.x; t < ncls * CF_LDS_STRIDE; t += blockDim.x) lct[t] = p.ctab[t];
         __syncthreads();
     }
-#if SHUD_ELE_PERSIST
-    // tiles of XCD x are [x*per_x, (x+1)*per_x); the gridDim/8 workgroups on XCD x stride through them
-    const int ntile = (n_compute - i0 + 255) >> 8;
-    const int per_x = (ntile + 7) >> 3;
-    const int x = blockIdx.x & 7, gx = gridDim.x >> 3;
-    for (int k = blockIdx.x >> 3; k < per_x; k += gx) {
-        const int i = i0 + ((x * per_x + k) << 8) + threadIdx.x;
-        if (i < n_compute) ele_body<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH>(m, p, Y, dy, i, cur, dg, lk, lct);
-    }
-#else
     const int i = i0 + block_id<1>() * blockDim.x + threadIdx.x;   // elements [i0, n_compute)
     if (i < n_compute) ele_body<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH>(m, p, Y, dy, i, cur, dg, lk, lct);
-#endif
 }
 
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
@@ -679,15 +664,6 @@ static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, doubl
     int nb = (i1 - i0 + 255) / 256;
     nb = (nb + 7) / 8 * 8;                  // block_id<1> deals blocks to XCDs in contiguous chunks
     const size_t lds = LCT ? (size_t)p.ncls * CF_LDS_STRIDE * sizeof(double) : 0;
-#if SHUD_ELE_PERSIST
-    static const int slots = [] {           // resident workgroups: CUs x (SHUD_ELE_WAVES x 4 SIMDs / 4 waves)
-        int dev = 0, cus = 256;
-        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        return cus * SHUD_ELE_WAVES;
-    }();
-    nb = std::min(nb, slots) / 8 * 8;
-    if (nb < 8) nb = 8;
-#endif
     hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH>), dim3(nb), dim3(256), lds, s, m, p,
                        Y, dy, i0, i1, cur, dg, lk);
 }

@@ -203,12 +203,14 @@ __global__ void __launch_bounds__(256) shud_et_kernel(DevEt e, EtStepDev s, DevE
     e.y_is[i] = icStg * vgFrac;
     e.y_snow[i] = snStg;
 
-    // ---- outputs: diagnostics + the RHS step inputs ----
-    e.t_prcp[i] = prcp; e.t_temp[i] = temp; e.t_lai[i] = lai; e.t_mf[i] = mf; e.t_rn[i] = rn;
-    e.t_wind[i] = wind; e.t_rh[i] = rh; e.rn_factor[i] = factor;
-    e.rn_h[i] = dswrf_h; e.rn_t[i] = dswrf_t;
-    e.q_prep[i] = prcp; e.q_pet[i] = qpet; e.q_ptr[i] = qptr; e.q_etp[i] = etp; e.q_netp[i] = netp;
-    e.q_eic[i] = eic; e.fu_surf[i] = fu_surf; e.fu_sub[i] = fu_sub;
+    // ---- outputs: diagnostics + the RHS step inputs (single-use streams: non-temporal stores) ----
+#define STN(p, v) __builtin_nontemporal_store((double)(v), &(p)[i])
+    STN(e.t_prcp, prcp); STN(e.t_temp, temp); STN(e.t_lai, lai); STN(e.t_mf, mf); STN(e.t_rn, rn);
+    STN(e.t_wind, wind); STN(e.t_rh, rh); STN(e.rn_factor, factor);
+    STN(e.rn_h, dswrf_h); STN(e.rn_t, dswrf_t);
+    STN(e.q_prep, prcp); STN(e.q_pet, qpet); STN(e.q_ptr, qptr); STN(e.q_etp, etp); STN(e.q_netp, netp);
+    STN(e.q_eic, eic); STN(e.fu_surf, fu_surf); STN(e.fu_sub, fu_sub);
+#undef STN
     if (s.packed) {                                   // the element kernel's records (shud_dev.h DevPacked)
         s.s_np[i] = make_double2(netp, qpet);
         s.s_tl[i] = make_double2(qptr, etp);
