@@ -82,6 +82,9 @@ inline bool cdiv_divisor_ok(double b) {
 #define SHUD_LDS_CLS_MAX 128
 #endif
 constexpr int kLdsClassMax = SHUD_LDS_CLS_MAX;
+// most classes a 1024-thread workgroup stages in LDS (600 x 33 x 8 B = 155 KiB of the CU's 160 KiB: one workgroup
+// per CU, 4 waves/SIMD) — models with 129..600 distinct parameter tuples
+constexpr int kLdsClassMaxBig = 600;
 
 struct DevPacked {
     const double *ctab;     // [ncls][CF_STRIDE] record-major: one class's fields share 2-3 cache lines
@@ -112,6 +115,7 @@ struct DevPacked {
     const double2 *rv;      // [4 * NR]
     const int4 *rv_i;       // {down, BC, first reach-sorted segment, #segments}
     const int4 *rv_u;       // {up0, up1, up2, #up} (ascending global order); #up = -1: use up_off/up_idx
+    int lds_big;            // 1: 129..kLdsClassMaxBig classes take the 1024-thread LDS-table kernel (host dispatch)
     // correctly rounded reciprocals of static geometric divisors, uploaded only for a kernel built with the
     // matching SHUD_RCP bit (shud_ele_rcp_mask()): 1 area, 2 Dist2Nabor [3][NE], 4 segment reach BedThick
     const double *r_area, *r_d2n, *sg_rbt;

@@ -114,6 +114,19 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     if (i < n_compute) ele_body<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH>(m, p, Y, dy, i, cur, dg, lk, lct);
 }
 
+// 129..kLdsClassMaxBig classes: the same body with the class table in LDS, staged by 1024-thread workgroups (one
+// per CU, 4 waves/SIMD) — instead of dependent L2 trips per class field (the L2 table) or the SoA layout
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool GH>
+__global__ void __launch_bounds__(1024, 4)
+shud_ele_kernel_packed_big(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int i0, int n_compute, int cur,
+                           DevDiag dg, DevLake lk) {
+    extern __shared__ double lct[];
+    for (int t = threadIdx.x; t < p.ncls * CF_LDS_STRIDE; t += blockDim.x) lct[t] = p.ctab[t];
+    __syncthreads();
+    const int i = i0 + block_id<1>() * blockDim.x + threadIdx.x;
+    if (i < n_compute) ele_body<MODE, OPEN, DIAG, FU1, true, false, GH>(m, p, Y, dy, i, cur, dg, lk, lct);
+}
+
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
 __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, const YView &Y, double *__restrict__ dy,
                                          int i, int cur, const DevDiag &dg, const DevLake &lk, const double *lct) {
@@ -658,6 +671,22 @@ shud_pack_step_kernel(DevMesh m, DevPacked p, int n, int cur, unsigned what) {
     if (what & 16) p.cs[cur][i].y = m.e_ic[0][i];
 }
 
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool GH>
+static void launch_big(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1, int cur,
+                       const DevDiag &dg, const DevLake &lk, hipStream_t s) {
+    int nb = (i1 - i0 + 1023) / 1024;
+    nb = (nb + 7) / 8 * 8;                  // block_id<1> deals blocks to XCDs in contiguous chunks
+    const size_t lds = (size_t)p.ncls * CF_LDS_STRIDE * sizeof(double);
+    auto *fn = shud_ele_kernel_packed_big<MODE, OPEN, DIAG, FU1, GH>;
+    static bool attr = false;               // dynamic LDS above 64 KiB must be allowed per kernel
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)(kLdsClassMaxBig * CF_LDS_STRIDE * sizeof(double)));
+        attr = true;
+    }
+    hipLaunchKernelGGL(fn, dim3(nb), dim3(1024), lds, s, m, p, Y, dy, i0, i1, cur, dg, lk);
+}
+
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
 static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1, int cur,
                      const DevDiag &dg, const DevLake &lk, hipStream_t s) {
@@ -682,6 +711,10 @@ void launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YV
         if (lake && MO == 0) {                                                                            \
             if (gh) launch_p<MO, OP, DI, FU, true, true, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s);      \
             else launch_p<MO, OP, DI, FU, true, true, false>(m, p, Y, dy, i0, i1, cur, dg, lk, s);        \
+        }                                                                                                 \
+        else if (p.ncls > LDS_CLS_MAX && p.ncls <= kLdsClassMaxBig && p.lds_big) {                        \
+            if (gh) launch_big<MO, OP, DI, FU, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s);                 \
+            else launch_big<MO, OP, DI, FU, false>(m, p, Y, dy, i0, i1, cur, dg, lk, s);                   \
         }                                                                                                 \
         else if (p.ncls <= LDS_CLS_MAX) {                                                                 \
             if (gh) launch_p<MO, OP, DI, FU, true, false, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s);     \

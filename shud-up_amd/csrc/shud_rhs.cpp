@@ -366,14 +366,16 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         cls[i] = it->second;
     }
     const int ncls = (int)table.size();
-    // beyond what one workgroup's LDS copy holds (128 classes) the class lookups become dependent L2 trips.
-    // Measured on syn-10M (tools/class_sweep.py, profiles/r02/class_sweep.log): element kernel 0.65 ms with
-    // 33 classes in LDS; from L2 0.83 ms at 132 classes, 1.21 at 495, 1.49 at 1,980, 1.66 at 13,200; the SoA
-    // kernel 1.09 ms at any count -> the L2 table up to 256 classes, SoA above (SHUD_RHS_L2_CLASS=1 forces the
-    // L2 table, =0 forces SoA above 128: A/B and bench.py many_class)
+    // beyond what a 256-thread workgroup's LDS copy holds (128 classes) the class table goes to 1024-thread
+    // workgroups (up to kLdsClassMaxBig = 600 classes, one per CU); beyond that the lookups would be dependent
+    // L2 trips.  Measured on syn-10M (tools/class_sweep.py, profiles/r02/class_sweep.log): element kernel 0.65 ms
+    // with 33 classes in LDS; from L2 0.83 ms at 132 classes, 1.21 at 495, 1.49 at 1,980, 1.66 at 13,200; the
+    // SoA kernel 1.09 ms at any count -> SoA above 600 (SHUD_RHS_L2_CLASS=1 forces the L2 table at any count and
+    // disables the 1024-thread LDS kernel, =0 forces SoA above 128: A/B and bench.py many_class)
     const char *l2 = getenv("SHUD_RHS_L2_CLASS");
-    const int l2_max = (l2 && l2[0] == '1') ? 32768 : (l2 && l2[0] == '0') ? kLdsClassMax : 256;
+    const int l2_max = (l2 && l2[0] == '1') ? 32768 : (l2 && l2[0] == '0') ? kLdsClassMax : kLdsClassMaxBig;
     if (ncls > l2_max) return 0;
+    h->dp.lds_big = (l2 && l2[0] == '1') ? 0 : 1;
     std::vector<double> ctab((size_t)CF_STRIDE * ncls, 0.0);
     for (int c = 0; c < ncls; c++) {
         std::vector<double> &t = table[c];

@@ -240,6 +240,22 @@ def test_many_classes(oracle_mod, monkeypatch, l2):
                           label=f"many-class l2={l2}", layout="packed" if l2 == "1" else "soa")
 
 
+def test_lds_big_class_table(oracle_mod, monkeypatch):
+    """129..600 distinct parameter tuples: the packed kernel with the class table staged in LDS by 1024-thread
+    workgroups (shud_ele_kernel_packed_big), serial and OMP semantics, against the oracle."""
+    monkeypatch.delenv("SHUD_RHS_L2_CLASS", raising=False)
+    rt = _runtime()
+    m, y = cases.variant(20000, seed=17)
+    m.par["KsatH"] = m.par["KsatH"] * (1.0 + 1e-7 * (np.arange(m.num_ele) % 12))     # 33 x 12 tuples
+    h = rt.RhsHandle(m)
+    lay = h.layout()
+    h.close()
+    assert lay["packed"] and 128 < lay["n_classes"] <= 600, lay
+    for mode in (abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP):
+        _compare_sequence(m, [y] + cases.states(m, None, 1, seed=3), mode, oracle_mod, ncalls=2,
+                          label=f"lds-big {lay['n_classes']} classes", layout="packed")
+
+
 @pytest.mark.parametrize("mode", [abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP])
 def test_edge_meshes(mode, oracle_mod, layout):
     """Edge cases of the mesh: no rivers at all (NR = NS = 0, empty river launch), the smallest synthetic meshes

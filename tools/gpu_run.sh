@@ -11,6 +11,7 @@
 #   sq           SQ / GRBM counter passes (tools/sq_counters.sh)          ode   integrator kernel trace
 #   part1        bench's N>1 code path on one rank                        rank  tools/rank_timing.py (2/4/8-way)
 #   e2e          tools/profile_e2e.sh 1M, 1 day                          redbench  tools/ode_red_bench (reduction forms)
+#   classes      tools/class_sweep.py (element kernel vs #parameter classes, LDS / L2 / SoA)
 #   test:EXPR    pytest -m gpu -k EXPR                                    traj  tests/diag_traj_day.py (ccw one day)
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -53,6 +54,7 @@ for step in "$@"; do
     rank) timeout -k 10 400 python tools/rank_timing.py > "$O/rank_timing.json" 2> "$O/rank_timing.err" ;;
     e2e) timeout -k 10 600 bash tools/profile_e2e.sh 1000000 1 > "$O/e2e.log" 2>&1 ;;
     traj) timeout -k 10 300 python tests/diag_traj_day.py "$O/traj_ccw_day.json" > "$O/traj_ccw_day.log" 2>&1 ;;
+    classes) timeout -k 10 600 python tools/class_sweep.py > "$O/class_sweep.log" 2>&1 ;;
     redbench) timeout -k 10 120 tools/ode_red_bench 31000000 30 > "$O/ode_red_bench.log" 2>&1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
