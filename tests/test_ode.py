@@ -114,3 +114,30 @@ def test_shud_rhs_through_integrator_deterministic():
     assert outs[0][1] == outs[1][1]
     st = outs[0][1]
     assert st["nst"] >= 6 and st["hlast"] <= 10.0 and st["ncfn"] == 0
+
+
+def test_device_reduction_order_restatement():
+    """The restated device reduction order (order 1: one entry per thread in 1024-thread blocks, 16-lane tree
+    over the wave partials, a 1024-thread finalize with 4 interleaved accumulators) is a faithful sum: on a
+    state of ~300 blocks with a ragged tail it integrates decayn with the same step/order decisions as CVODE's
+    serial order and agrees to rounding.  (Bit-identity of order 1 with the device, up to 2.1M entries:
+    tests/test_gpu_ode.py, tests/test_gpu_properties.py.)"""
+    n = 300 * 1024 + 37
+    lam = np.array([0.01, 0.1, 1.0, 10.0, 100.0, 1000.0, 10000.0])[np.arange(n) % 7]
+    y0 = 1.0 + 0.5 * np.sin(np.arange(n))
+    res = {}
+    try:
+        for order in (0, 1):
+            oracle.OracleOde.set_reduction_order(order)
+            o = oracle.OracleOde("decayn", 0.0, y0, 1e-6, 1e-10, 1e-5, 0.0, 0.0)
+            flag, t, y = o.solve(0.002)
+            res[order] = (flag, t, y, o.stats())
+    finally:
+        oracle.OracleOde.set_reduction_order(0)
+    (f0, t0, y0_, s0), (f1, t1, y1, s1) = res[0], res[1]
+    assert f0 == f1 == 0 and t0 == t1
+    for k in ("nst", "nfe", "nni", "nli", "qcur"):
+        assert s0[k] == s1[k], k
+    assert np.all(np.abs(y1 - y0_) <= 1e-9 * np.abs(y0_) + 1e-15)
+    ex = y0 * np.exp(-lam * 0.002)
+    assert np.all(np.abs(y1 - ex) <= 2e-4 * np.abs(ex) + 1e-8)
