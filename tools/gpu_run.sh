@@ -23,6 +23,9 @@ for step in "$@"; do
   case "$step" in
     suite) timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --durations=30 --timeout 240 --timeout-method thread > "$O/pytest_gpu.log" 2>&1 ;;
     test:*) timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread -k "${step#test:}" > "$O/pytest_sel.log" 2>&1 ;;
+    abtest:*)                   # abtest:LIB:EXPR  -> pytest -m gpu -k EXPR against build/ab/libshud_rhs_LIB.so
+      rest="${step#abtest:}"; lib="${rest%%:*}"; expr="${rest#*:}"
+      SHUD_RHS_LIB=$PWD/shud-up_amd/build/ab/libshud_rhs_$lib.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread -k "$expr" > "$O/pytest_ab_$lib.log" 2>&1 ;;
     smoke) timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 ;;
     bench) timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > "$O/bench.json" 2> "$O/bench.err" ;;
     quick) timeout -k 10 300 python bench.py $A --steps 20 --warmup 5 > "$O/quick.json" 2> "$O/quick.err" ;;
