@@ -90,25 +90,8 @@ constexpr int CF_LDS_STRIDE = CF_STRIDE;   // the HBM table's record layout, cop
 // fun_Ele_lakeVertical / fun_Ele_lakeHorizon (Element.cpp:336-346, MD_ElementFlux.cpp:2-23) and get zero DY
 // (MD_f.cpp:146-150); bank edges of other elements exchange with the lake (MD_ElementFlux.cpp:46-53,107-121)
 // and leave their fluxes in DevLake for the lake kernel.  LAKE = false compiles all of it away.
-// SHUD_NB_LDS (A/B): the three neighbours' {z_surf, z_bottom}, class word and sf / gw states are gathered
-// straight into LDS by global_load_lds (no VGPRs held while in flight) right after the element's own record,
-// so they arrive during the vertical physics instead of stalling each edge iteration; 2,304 B per wave per edge
-#ifndef SHUD_NB_LDS
-#define SHUD_NB_LDS 0
-#endif
-constexpr int kNbJ = 2304;              // per wave and edge: zz 64x16 | cf 64x4 | sf lo, hi | gw lo, hi (64x4 each)
-constexpr int kNbBlock = 4 * 3 * kNbJ;  // per 256-thread workgroup
 #ifndef SHUD_ELE_WAVES
-#define SHUD_ELE_WAVES (SHUD_NB_LDS ? 4 : 5)   // min waves per SIMD: <= 96 VGPRs (rolled edge loop, no spills)
-#endif
-#if SHUD_NB_LDS
-typedef __attribute__((address_space(3))) char lds_char;
-__device__ __forceinline__ void dma16(const void *g, lds_char *l) {
-    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)l, 16, 0, 0);
-}
-__device__ __forceinline__ void dma4(const void *g, lds_char *l) {
-    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)l, 4, 0, 0);
-}
+#define SHUD_ELE_WAVES 5        // min waves per SIMD: <= 96 VGPRs (rolled edge loop, no spills)
 #endif
 // One 256-element tile per workgroup.  (Persistent workgroups — one per resident slot looping over XCD-chunked
 // tiles, the class table copied to LDS once per workgroup — measured 0.735 vs 0.657 ms: the tile loop took the
@@ -160,25 +143,6 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     const int cf = mt.w;
     const int cid = cf_class(cf), ibc = cf_ibc(cf);
     const bool is_lake = LAKE && cf < 0;
-#if SHUD_NB_LDS
-    extern __shared__ double lds_dyn[];
-    lds_char *const nbw = (lds_char *)(lds_dyn + ((p.ncls * CF_LDS_STRIDE + 1) & ~1)) + (threadIdx.x >> 6) * (3 * kNbJ);
-#pragma unroll
-    for (int j = 0; j < 3; j++) {
-        const int nbj = j == 0 ? mt.x : j == 1 ? mt.y : mt.z;
-        const int nc = nbj >= 0 ? nbj : i;
-        lds_char *r = nbw + j * kNbJ;
-        dma16(p.zz + nc, r);
-        dma4((const int *)(p.meta + nc) + 3, r + 1024);
-        const double *ps = GH ? (nc < nown ? Y.y + nc : Y.gele + 3 * (nc - nown)) : Y.y + nc;
-        const double *pg = GH ? (nc < nown ? Y.y + 2 * (size_t)nown + nc : Y.gele + 3 * (nc - nown) + 2)
-                              : Y.y + 2 * (size_t)nown + nc;
-        dma4(ps, r + 1280);
-        dma4((const int *)ps + 1, r + 1536);
-        dma4(pg, r + 1792);
-        dma4((const int *)pg + 1, r + 2048);
-    }
-#endif
     const double2 snp = ldnt2(at(p.s_np, o16)), stl = ldnt2(at(p.s_tl, o16));   // stl = {pot_tran, ETP}
     const double etp = stl.y;
     double2 fu;
@@ -340,25 +304,11 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
         const int nb = j == 0 ? mt.x : j == 1 ? mt.y : mt.z;
         const double2 g = ldnt2(at(p.ged + (size_t)j * NEl, o16));
         const int nc = nb >= 0 ? nb : i;                  // boundary edge: harmless in-bounds loads
-#if SHUD_NB_LDS
-        if (j == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the neighbour DMA has landed
-        const lds_char *r = nbw + j * kNbJ;
-        const int lane = threadIdx.x & 63;
-        const v2d nzv = *(const __attribute__((address_space(3))) v2d *)(r + 16 * lane);
-        const double2 nzz = make_double2(nzv.x, nzv.y);
-        const int ncf = *(const __attribute__((address_space(3))) int *)(r + 1024 + 4 * lane);
-        const double nsf_raw = __hiloint2double(*(const __attribute__((address_space(3))) int *)(r + 1536 + 4 * lane),
-                                                *(const __attribute__((address_space(3))) int *)(r + 1280 + 4 * lane));
-        const double ngw_raw = __hiloint2double(*(const __attribute__((address_space(3))) int *)(r + 2048 + 4 * lane),
-                                                *(const __attribute__((address_space(3))) int *)(r + 1792 + 4 * lane));
-        (void)nc;
-#else
         const uint32_t n16 = (uint32_t)nc << 4, n8 = (uint32_t)nc << 3;
         const double2 nzz = *at(p.zz, n16);
         const int ncf = *at((const int *)p.meta + 3, n16);
         const double nsf_raw = GH ? Y.sf(nc) : *at(Y.y, n8);
         const double ngw_raw = GH ? Y.gw(nc) : *at(Y.y + 2 * (size_t)nown, n8);
-#endif
         const double B = g.x, d2n = g.y;
 #if SHUD_RCP & 2
         const double rd2n = ldnt(at(p.r_d2n + (size_t)j * NEl, o8));
@@ -742,10 +692,7 @@ static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, doubl
                      const DevDiag &dg, const DevLake &lk, hipStream_t s) {
     int nb = (i1 - i0 + 255) / 256;
     nb = (nb + 7) / 8 * 8;                  // block_id<1> deals blocks to XCDs in contiguous chunks
-    size_t lds = LCT ? (size_t)p.ncls * CF_LDS_STRIDE * sizeof(double) : 0;
-#if SHUD_NB_LDS
-    lds = (size_t)((p.ncls * CF_LDS_STRIDE + 1) & ~1) * sizeof(double) + kNbBlock;
-#endif
+    const size_t lds = LCT ? (size_t)p.ncls * CF_LDS_STRIDE * sizeof(double) : 0;
     hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH>), dim3(nb), dim3(256), lds, s, m, p,
                        Y, dy, i0, i1, cur, dg, lk);
 }
