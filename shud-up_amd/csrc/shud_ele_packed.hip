@@ -96,22 +96,80 @@ constexpr int CF_LDS_STRIDE = CF_STRIDE;   // the HBM table's record layout, cop
 // One 256-element tile per workgroup.  (Persistent workgroups — one per resident slot looping over XCD-chunked
 // tiles, the class table copied to LDS once per workgroup — measured 0.735 vs 0.657 ms: the tile loop took the
 // kernel to 96 VGPRs with spills, profiles/r03/ab_persist/.)
+// SHUD_EDGE0_PF: prefetch edge 0's neighbour data right after the own record (A/B)
+#ifndef SHUD_EDGE0_PF
+#define SHUD_EDGE0_PF 0
+#endif
+// the element's own records, loaded before the workgroup's class-table barrier so both round trips overlap
+struct OwnRec {
+    int4 mt;
+    double2 zz, snp, stl, fu, csv;
+    double ysf, yus, ygw;
+};
+template <bool FU1, bool GH>
+__device__ __forceinline__ OwnRec load_own(const DevPacked &p, const YView &Y, int i, int cur) {
+    const int nown = Y.n_own;
+    const uint32_t o16 = (uint32_t)i << 4, o8 = (uint32_t)i << 3;
+    OwnRec o;
+    o.mt = *at(p.meta, o16);
+    o.zz = *at(p.zz, o16);
+    o.ysf = GH ? Y.sf(i) : *at(Y.y, o8);
+    o.yus = GH ? Y.us(i) : *at(Y.y + nown, o8);
+    o.ygw = GH ? Y.gw(i) : *at(Y.y + 2 * (size_t)nown, o8);
+    o.snp = ldnt2(at(p.s_np, o16));
+    o.stl = ldnt2(at(p.s_tl, o16));                       // {pot_tran, ETP}
+    if (FU1) { o.fu.x = 1.0; o.fu.y = 1.0; } else o.fu = ldnt2(at(p.s_fu, o16));
+    o.csv = ldnt2(at(p.cs[cur], o16));
+    return o;
+}
+// class table global -> LDS by BS threads: the first kTabBatch loads of every thread are issued together (and
+// before the caller's own-record loads, which they overlap), then stored; a longer table continues in a loop.
+// (A load -> wait -> ds_write per iteration cost one L2 round trip per 256 table words at every workgroup start.)
+constexpr int kTabBatch = 8;
+template <int BS>
+__device__ __forceinline__ void tab_issue(const DevPacked &p, double (&tv)[kTabBatch]) {
+    const int nt = p.ncls * CF_LDS_STRIDE;
+#pragma unroll
+    for (int k = 0; k < kTabBatch; k++) {
+        const int t = (int)threadIdx.x + k * BS;
+        tv[k] = t < nt ? p.ctab[t] : 0.;
+    }
+}
+template <int BS>
+__device__ __forceinline__ void tab_store(const DevPacked &p, const double (&tv)[kTabBatch], double *lct) {
+    const int nt = p.ncls * CF_LDS_STRIDE;
+#pragma unroll
+    for (int k = 0; k < kTabBatch; k++) {
+        const int t = (int)threadIdx.x + k * BS;
+        if (t < nt) lct[t] = tv[k];
+    }
+    for (int t = (int)threadIdx.x + kTabBatch * BS; t < nt; t += BS) lct[t] = p.ctab[t];
+}
+// workgroup -> tile: XCD-contiguous chunks (block_id<1>, shud_physics.h) with the chunk length per8 = grid/8
+// passed by the launcher, so no workgroup reads the grid size from the dispatch packet at its start
+__device__ __forceinline__ int tile_of(int per8) { return (int)(blockIdx.x & 7) * per8 + (int)(blockIdx.x >> 3); }
+
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
 __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, const YView &Y, double *__restrict__ dy,
-                                         int i, int cur, const DevDiag &dg, const DevLake &lk, const double *lct);
+                                         int i, int cur, const DevDiag &dg, const DevLake &lk, const double *lct,
+                                         const OwnRec &own);
 
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
 __global__ void __launch_bounds__(256, SHUD_ELE_WAVES)
 shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int i0, int n_compute, int cur,
-                       DevDiag dg, DevLake lk) {
+                       DevDiag dg, DevLake lk, int per8) {
     extern __shared__ double lct[];                       // ncls * CF_LDS_STRIDE doubles when LCT
-    const int ncls = p.ncls;
+    const int i = i0 + tile_of(per8) * 256 + (int)threadIdx.x;   // elements [i0, n_compute)
+    const bool act = i < n_compute;
+    double tv[kTabBatch];
+    if (LCT) tab_issue<256>(p, tv);
+    OwnRec own;
+    if (act) own = load_own<FU1, GH>(p, Y, i, cur);
     if (LCT) {
-        for (int t = threadIdx.x; t < ncls * CF_LDS_STRIDE; t += blockDim.x) lct[t] = p.ctab[t];
+        tab_store<256>(p, tv, lct);
         __syncthreads();
     }
-    const int i = i0 + block_id<1>() * blockDim.x + threadIdx.x;   // elements [i0, n_compute)
-    if (i < n_compute) ele_body<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH>(m, p, Y, dy, i, cur, dg, lk, lct);
+    if (act) ele_body<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH>(m, p, Y, dy, i, cur, dg, lk, lct, own);
 }
 
 // 129..kLdsClassMaxBig classes: the same body with the class table in LDS, staged by 1024-thread workgroups (one
@@ -119,35 +177,50 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool GH>
 __global__ void __launch_bounds__(1024, 4)
 shud_ele_kernel_packed_big(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int i0, int n_compute, int cur,
-                           DevDiag dg, DevLake lk) {
+                           DevDiag dg, DevLake lk, int per8) {
     extern __shared__ double lct[];
-    for (int t = threadIdx.x; t < p.ncls * CF_LDS_STRIDE; t += blockDim.x) lct[t] = p.ctab[t];
+    const int i = i0 + tile_of(per8) * 1024 + (int)threadIdx.x;
+    const bool act = i < n_compute;
+    double tv[kTabBatch];
+    tab_issue<1024>(p, tv);
+    OwnRec own;
+    if (act) own = load_own<FU1, GH>(p, Y, i, cur);
+    tab_store<1024>(p, tv, lct);
     __syncthreads();
-    const int i = i0 + block_id<1>() * blockDim.x + threadIdx.x;
-    if (i < n_compute) ele_body<MODE, OPEN, DIAG, FU1, true, false, GH>(m, p, Y, dy, i, cur, dg, lk, lct);
+    if (act) ele_body<MODE, OPEN, DIAG, FU1, true, false, GH>(m, p, Y, dy, i, cur, dg, lk, lct, own);
 }
 
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
 __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, const YView &Y, double *__restrict__ dy,
-                                         int i, int cur, const DevDiag &dg, const DevLake &lk, const double *lct) {
+                                         int i, int cur, const DevDiag &dg, const DevLake &lk, const double *lct,
+                                         const OwnRec &own) {
     const int NEl = m.num_ele;
     const int nown = Y.n_own;
-    // ---------------- own records first; saturation (its two pow calls are the register peak) is computed
-    // while little else is live ----------------
+    // ---------------- own records (loaded by the caller); saturation (its two pow calls are the register peak) is
+    // computed while little else is live ----------------
     const uint32_t o16 = (uint32_t)i << 4, o8 = (uint32_t)i << 3;
-    const int4 mt = *at(p.meta, o16);
-    const double2 zz = *at(p.zz, o16);
-    const double ysf_raw = GH ? Y.sf(i) : *at(Y.y, o8);
-    const double yus_raw = GH ? Y.us(i) : *at(Y.y + nown, o8);
-    const double ygw_raw = GH ? Y.gw(i) : *at(Y.y + 2 * (size_t)nown, o8);
+    (void)o16;
+    const int4 mt = own.mt;
+    const double2 zz = own.zz;
+    const double ysf_raw = own.ysf, yus_raw = own.yus, ygw_raw = own.ygw;
     const int cf = mt.w;
     const int cid = cf_class(cf), ibc = cf_ibc(cf);
     const bool is_lake = LAKE && cf < 0;
-    const double2 snp = ldnt2(at(p.s_np, o16)), stl = ldnt2(at(p.s_tl, o16));   // stl = {pot_tran, ETP}
+#if SHUD_EDGE0_PF
+    // edge 0's neighbour data and geometry, issued as soon as the own record is in: in flight during the
+    // vertical physics instead of stalling the first edge iteration
+    const int nc0 = mt.x >= 0 ? mt.x : i;
+    const uint32_t n16_0 = (uint32_t)nc0 << 4, n8_0 = (uint32_t)nc0 << 3;
+    const double2 pf_zz = *at(p.zz, n16_0);
+    const int pf_cf = *at((const int *)p.meta + 3, n16_0);
+    const double pf_sf = GH ? Y.sf(nc0) : *at(Y.y, n8_0);
+    const double pf_gw = GH ? Y.gw(nc0) : *at(Y.y + 2 * (size_t)nown, n8_0);
+    const double2 pf_g = ldnt2(at(p.ged, o16));
+#endif
+    const double2 snp = own.snp, stl = own.stl;            // stl = {pot_tran, ETP}
     const double etp = stl.y;
-    double2 fu;
-    if (FU1) { fu.x = 1.0; fu.y = 1.0; } else fu = ldnt2(at(p.s_fu, o16));
-    const double2 csv = ldnt2(at(p.cs[cur], o16));
+    const double2 fu = own.fu;
+    const double2 csv = own.csv;
 #define CL(f) (LCT ? lct[cid * CF_LDS_STRIDE + CF_##f] : p.ctab[cid * CF_STRIDE + CF_##f])
 #define CDIV(a, F) CDIV_(a, CL(F), CL(r_##F))
 
@@ -302,13 +375,23 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
 #pragma unroll 1
     for (int j = 0; j < (is_lake ? 0 : 3); j++) {     // lake elements: fun_Ele_lakeHorizon, all zero
         const int nb = j == 0 ? mt.x : j == 1 ? mt.y : mt.z;
-        const double2 g = ldnt2(at(p.ged + (size_t)j * NEl, o16));
         const int nc = nb >= 0 ? nb : i;                  // boundary edge: harmless in-bounds loads
-        const uint32_t n16 = (uint32_t)nc << 4, n8 = (uint32_t)nc << 3;
-        const double2 nzz = *at(p.zz, n16);
-        const int ncf = *at((const int *)p.meta + 3, n16);
-        const double nsf_raw = GH ? Y.sf(nc) : *at(Y.y, n8);
-        const double ngw_raw = GH ? Y.gw(nc) : *at(Y.y + 2 * (size_t)nown, n8);
+        double2 g, nzz;
+        int ncf;
+        double nsf_raw, ngw_raw;
+#if SHUD_EDGE0_PF
+        if (j == 0) {
+            g = pf_g; nzz = pf_zz; ncf = pf_cf; nsf_raw = pf_sf; ngw_raw = pf_gw;
+        } else
+#endif
+        {
+            const uint32_t n16 = (uint32_t)nc << 4, n8 = (uint32_t)nc << 3;
+            g = ldnt2(at(p.ged + (size_t)j * NEl, o16));
+            nzz = *at(p.zz, n16);
+            ncf = *at((const int *)p.meta + 3, n16);
+            nsf_raw = GH ? Y.sf(nc) : *at(Y.y, n8);
+            ngw_raw = GH ? Y.gw(nc) : *at(Y.y + 2 * (size_t)nown, n8);
+        }
         const double B = g.x, d2n = g.y;
 #if SHUD_RCP & 2
         const double rd2n = ldnt(at(p.r_d2n + (size_t)j * NEl, o8));
@@ -470,10 +553,10 @@ __device__ __forceinline__ double riv_down_outlet(const RivP &q, double uq, cons
 #endif
 template <int MODE, bool DIAG, int ABL = 0>
 __global__ void __launch_bounds__(256)
-shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, DevDiag dg) {
+shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, DevDiag dg, int per8) {
     // XCD-chunked workgroup order: a reach's up/downstream records sit a few blocks away in index space,
     // so they are L2 hits on the same XCD instead of fabric round trips (speed only)
-    const int r = block_id<1>() * blockDim.x + threadIdx.x;
+    const int r = tile_of(per8) * 256 + (int)threadIdx.x;
     if (r >= Y.n_own_riv) return;
     const RivP q = riv_load(p, r);
     const int4 ii = p.rv_i[r];                                  // {down, BC, first segment, #segments}
@@ -558,16 +641,16 @@ void launch_river_kernel_packed(const DevMesh &m, const DevPacked &p, const YVie
 #if SHUD_RIV_ABL
     // timing-only ablation build (tools/riv_abl.sh: -DSHUD_RIV_ABL=k); never part of the production library
     if (mode == 0 && !diag) {
-        hipLaunchKernelGGL((shud_riv_kernel_packed<0, false, SHUD_RIV_ABL>), grid, blk, 0, s, m, p, Y, dy, dg);
+        hipLaunchKernelGGL((shud_riv_kernel_packed<0, false, SHUD_RIV_ABL>), grid, blk, 0, s, m, p, Y, dy, dg, (int)grid.x / 8);
         return;
     }
 #endif
     if (mode == 0) {
-        if (diag) hipLaunchKernelGGL((shud_riv_kernel_packed<0, true>), grid, blk, 0, s, m, p, Y, dy, dg);
-        else hipLaunchKernelGGL((shud_riv_kernel_packed<0, false>), grid, blk, 0, s, m, p, Y, dy, dg);
+        if (diag) hipLaunchKernelGGL((shud_riv_kernel_packed<0, true>), grid, blk, 0, s, m, p, Y, dy, dg, (int)grid.x / 8);
+        else hipLaunchKernelGGL((shud_riv_kernel_packed<0, false>), grid, blk, 0, s, m, p, Y, dy, dg, (int)grid.x / 8);
     } else {
-        if (diag) hipLaunchKernelGGL((shud_riv_kernel_packed<1, true>), grid, blk, 0, s, m, p, Y, dy, dg);
-        else hipLaunchKernelGGL((shud_riv_kernel_packed<1, false>), grid, blk, 0, s, m, p, Y, dy, dg);
+        if (diag) hipLaunchKernelGGL((shud_riv_kernel_packed<1, true>), grid, blk, 0, s, m, p, Y, dy, dg, (int)grid.x / 8);
+        else hipLaunchKernelGGL((shud_riv_kernel_packed<1, false>), grid, blk, 0, s, m, p, Y, dy, dg, (int)grid.x / 8);
     }
 }
 
@@ -684,7 +767,7 @@ static void launch_big(const DevMesh &m, const DevPacked &p, const YView &Y, dou
                                   (int)(kLdsClassMaxBig * CF_LDS_STRIDE * sizeof(double)));
         attr = true;
     }
-    hipLaunchKernelGGL(fn, dim3(nb), dim3(1024), lds, s, m, p, Y, dy, i0, i1, cur, dg, lk);
+    hipLaunchKernelGGL(fn, dim3(nb), dim3(1024), lds, s, m, p, Y, dy, i0, i1, cur, dg, lk, nb / 8);
 }
 
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
@@ -694,7 +777,7 @@ static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, doubl
     nb = (nb + 7) / 8 * 8;                  // block_id<1> deals blocks to XCDs in contiguous chunks
     const size_t lds = LCT ? (size_t)p.ncls * CF_LDS_STRIDE * sizeof(double) : 0;
     hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH>), dim3(nb), dim3(256), lds, s, m, p,
-                       Y, dy, i0, i1, cur, dg, lk);
+                       Y, dy, i0, i1, cur, dg, lk, nb / 8);
 }
 
 void launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1,
