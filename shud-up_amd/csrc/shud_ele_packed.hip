@@ -96,10 +96,6 @@ constexpr int CF_LDS_STRIDE = CF_STRIDE;   // the HBM table's record layout, cop
 // One 256-element tile per workgroup.  (Persistent workgroups — one per resident slot looping over XCD-chunked
 // tiles, the class table copied to LDS once per workgroup — measured 0.735 vs 0.657 ms: the tile loop took the
 // kernel to 96 VGPRs with spills, profiles/r03/ab_persist/.)
-// SHUD_EDGE0_PF: prefetch edge 0's neighbour data right after the own record (A/B)
-#ifndef SHUD_EDGE0_PF
-#define SHUD_EDGE0_PF 0
-#endif
 // the element's own records, loaded before the workgroup's class-table barrier so both round trips overlap
 struct OwnRec {
     int4 mt;
@@ -206,17 +202,6 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     const int cf = mt.w;
     const int cid = cf_class(cf), ibc = cf_ibc(cf);
     const bool is_lake = LAKE && cf < 0;
-#if SHUD_EDGE0_PF
-    // edge 0's neighbour data and geometry, issued as soon as the own record is in: in flight during the
-    // vertical physics instead of stalling the first edge iteration
-    const int nc0 = mt.x >= 0 ? mt.x : i;
-    const uint32_t n16_0 = (uint32_t)nc0 << 4, n8_0 = (uint32_t)nc0 << 3;
-    const double2 pf_zz = *at(p.zz, n16_0);
-    const int pf_cf = *at((const int *)p.meta + 3, n16_0);
-    const double pf_sf = GH ? Y.sf(nc0) : *at(Y.y, n8_0);
-    const double pf_gw = GH ? Y.gw(nc0) : *at(Y.y + 2 * (size_t)nown, n8_0);
-    const double2 pf_g = ldnt2(at(p.ged, o16));
-#endif
     const double2 snp = own.snp, stl = own.stl;            // stl = {pot_tran, ETP}
     const double etp = stl.y;
     const double2 fu = own.fu;
@@ -376,22 +361,14 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     for (int j = 0; j < (is_lake ? 0 : 3); j++) {     // lake elements: fun_Ele_lakeHorizon, all zero
         const int nb = j == 0 ? mt.x : j == 1 ? mt.y : mt.z;
         const int nc = nb >= 0 ? nb : i;                  // boundary edge: harmless in-bounds loads
-        double2 g, nzz;
-        int ncf;
-        double nsf_raw, ngw_raw;
-#if SHUD_EDGE0_PF
-        if (j == 0) {
-            g = pf_g; nzz = pf_zz; ncf = pf_cf; nsf_raw = pf_sf; ngw_raw = pf_gw;
-        } else
-#endif
-        {
-            const uint32_t n16 = (uint32_t)nc << 4, n8 = (uint32_t)nc << 3;
-            g = ldnt2(at(p.ged + (size_t)j * NEl, o16));
-            nzz = *at(p.zz, n16);
-            ncf = *at((const int *)p.meta + 3, n16);
-            nsf_raw = GH ? Y.sf(nc) : *at(Y.y, n8);
-            ngw_raw = GH ? Y.gw(nc) : *at(Y.y + 2 * (size_t)nown, n8);
-        }
+        // (edge 0's loads issued right after the own record instead — held through the vertical physics — took
+        // the kernel to 96 VGPRs with spills and measured 0.707 vs 0.617 ms, profiles/r03/ab_prologue/)
+        const uint32_t n16 = (uint32_t)nc << 4, n8 = (uint32_t)nc << 3;
+        const double2 g = ldnt2(at(p.ged + (size_t)j * NEl, o16));
+        const double2 nzz = *at(p.zz, n16);
+        const int ncf = *at((const int *)p.meta + 3, n16);
+        const double nsf_raw = GH ? Y.sf(nc) : *at(Y.y, n8);
+        const double ngw_raw = GH ? Y.gw(nc) : *at(Y.y + 2 * (size_t)nown, n8);
         const double B = g.x, d2n = g.y;
 #if SHUD_RCP & 2
         const double rd2n = ldnt(at(p.r_d2n + (size_t)j * NEl, o8));
