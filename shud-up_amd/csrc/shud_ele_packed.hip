@@ -67,6 +67,11 @@ __device__ __forceinline__ bool bad_nonneg(double x) {
     return __builtin_isfpclass(x, 0x0003 | 0x0004 | 0x0008 | 0x0010 | 0x0200);
 }
 
+// stage of an owned or ghost reach: the address is selected, so one load and no branch
+__device__ __forceinline__ const double *riv_y_at(const YView &Y, int r) {
+    return r < Y.n_own_riv ? Y.y + 3 * (size_t)Y.n_own + r : Y.griv + (r - Y.n_own_riv);
+}
+
 // packed cf word (DevPacked::meta.w)
 __device__ __forceinline__ int cf_ibc(int cf) { return (int)(int8_t)(cf & 0xff); }
 __device__ __forceinline__ int cf_iss(int cf) { return (cf >> 8) & 3; }
@@ -101,6 +106,7 @@ struct OwnRec {
     int4 mt;
     double2 zz, snp, stl, fu, csv;
     double ysf, yus, ygw;
+    int sfl;                                              // seg_first word (bit 31: LAI on)
 };
 template <bool FU1, bool GH>
 __device__ __forceinline__ OwnRec load_own(const DevPacked &p, const YView &Y, int i, int cur) {
@@ -116,8 +122,10 @@ __device__ __forceinline__ OwnRec load_own(const DevPacked &p, const YView &Y, i
     o.stl = ldnt2(at(p.s_tl, o16));                       // {pot_tran, ETP}
     if (FU1) { o.fu.x = 1.0; o.fu.y = 1.0; } else o.fu = ldnt2(at(p.s_fu, o16));
     o.csv = ldnt2(at(p.cs[cur], o16));
+    o.sfl = *at(p.seg_first, (uint32_t)i << 2);
     return o;
 }
+
 // class table global -> LDS by BS threads: the first kTabBatch loads of every thread are issued together (and
 // before the caller's own-record loads, which they overlap), then stored; a longer table continues in a loop.
 // (A load -> wait -> ds_write per iteration cost one L2 round trip per 256 table words at every workgroup start.)
@@ -234,7 +242,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
         }
     }
 
-    const int sfl = *at(p.seg_first, (uint32_t)i << 2);
+    const int sfl = own.sfl;
     const int sfirst = sfl & 0x7fffffff;
     const bool lai_on = sfl < 0;                       // bit 31: t_lai > ZERO (set with the step inputs)
     const int iss = cf_iss(cf), nseg = cf_nseg(cf);
@@ -325,6 +333,8 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
             const double2 lc = *at(p.sg_lc, k16), dk = *at(p.sg_dk, k16);
             const int2 rb = *at(p.sg_rb, k8);
             const double bt = *at(p.sg_bt, k8);
+            // (the first segment's reach index + stage loaded at the top of the body instead, in flight across the
+            // vertical physics: 88 VGPRs, 0.625 vs 0.623 ms — not kept, profiles/r03/ab_river2/)
             double yr = GH ? Y.riv(rb.x) : *at(Y.y + 3 * (size_t)nown, (uint32_t)rb.x << 3);   // uriv_of, BC below
             if (MODE == 1) yr = (yr >= 0.) ? yr : 0.;
             if (rb.y > 0) yr = m.rybc[rb.y];
@@ -528,6 +538,119 @@ __device__ __forceinline__ double riv_down_outlet(const RivP &q, double uq, cons
 #ifndef SHUD_RIV_ABL
 #define SHUD_RIV_ABL 0
 #endif
+// SHUD_RIV_V: 1 = one chain per neighbour (production), 2 = dependence-ordered loads (A/B)
+#ifndef SHUD_RIV_V
+#define SHUD_RIV_V 1
+#endif
+// f_update's clamp (MODE 1) and the BC override on an already loaded stage; *yg = what updateRiver() saw
+template <int MODE>
+__device__ __forceinline__ double riv_stage_v(double yr, int bc, double ybc, double *yg) {
+    if (MODE == 1) yr = (yr >= 0.) ? yr : 0.;
+    *yg = yr;
+    return bc > 0 ? ybc : yr;
+}
+#if SHUD_RIV_V == 2
+constexpr int kRivSegBatch = 8;
+// A reach's operands form a three-level dependence chain: its own record and index words; then its downstream
+// and up to 3 upstream reaches' records and stages and its segments' flux positions; then the segment fluxes.
+// Every load of a level is issued before any of the level's values is used (lanes without an upstream reach
+// masked off: a clamped always-on record load costs the scattered-access path as much as a real one), so a
+// reach costs three memory round trips instead of one per upstream reach and per branch (round 2: ~7 in series).
+// The physics and every sum's order are unchanged.
+template <int MODE, bool DIAG, int ABL = 0>
+__global__ void __launch_bounds__(256)
+shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, DevDiag dg, int per8) {
+    // XCD-chunked workgroup order: a reach's up/downstream records sit a few blocks away in index space,
+    // so they are L2 hits on the same XCD instead of fabric round trips (speed only)
+    const int r = tile_of(per8) * 256 + (int)threadIdx.x;
+    if (r >= Y.n_own_riv) return;
+    // ---- level 1 ----
+    const RivP q = riv_load(p, r);
+    const int4 ii = p.rv_i[r];                                  // {down, BC, first segment, #segments}
+    const int4 up = p.rv_u[r];                                  // {up0, up1, up2, #upstream or -1: CSR}
+    const double yr0 = Y.y[3 * (size_t)Y.n_own + r];
+    // ---- level 2 ----
+    const int d = (!(ABL & 4) && q.down >= 0) ? q.down : r;
+    const int nup = (ABL & 1) ? 0 : up.w;
+    const double2 bd = p.rv[4 * (size_t)d + 1], dd = p.rv[4 * (size_t)d + 3];   // same line of d's record
+    const double yd0 = *riv_y_at(Y, d);
+    RivP qu0, qu1, qu2;
+    double yu0 = 0., yu1 = 0., yu2 = 0.;
+    if (nup > 0) { qu0 = riv_load(p, up.x); yu0 = *riv_y_at(Y, up.x); }
+    if (nup > 1) { qu1 = riv_load(p, up.y); yu1 = *riv_y_at(Y, up.y); }
+    if (nup > 2) { qu2 = riv_load(p, up.z); yu2 = *riv_y_at(Y, up.z); }
+    const double ybc = m.rybc[q.bc > 0 ? q.bc : 0];             // tables hold >= 1 entry
+    const double qbc0 = m.rqbc[q.bc < 0 ? -q.bc : 0];
+    const int ns = (ABL & 2) ? 0 : ii.w;
+    const bool rsort = p.seg_rpos != nullptr;                   // reach-sorted fluxes: contiguous from ii.z
+    int ps[kRivSegBatch];
+#pragma unroll
+    for (int j = 0; j < kRivSegBatch; j++) {   // past the reach's last segment: its first again (same line)
+        const int k = ns > 0 ? ii.z + (j < ns ? j : 0) : 0;
+        ps[j] = rsort ? k : m.rseg_pos[k];
+    }
+    // ---- level 3 ----
+    double2 qv[kRivSegBatch];
+#pragma unroll
+    for (int j = 0; j < kRivSegBatch; j++) qv[j] = p.qseg2[ns > 0 ? ps[j] : 0];
+
+    double yg;
+    const double ur = riv_stage_v<MODE>(yr0, q.bc, ybc, &yg);
+    const RivGeom g = riv_geom_p(q, yg);
+    double qdown = 0.;
+    if (!(ABL & 4)) {
+        const int bcd = rv_ib(dd.y).y;
+        const double ydb = bcd > 0 ? m.rybc[bcd] : 0.;
+        double ydg;
+        const double ud = riv_stage_v<MODE>(yd0, bcd, ydb, &ydg);
+        qdown = riv_down_p(q, ur, g, ud, dd.x, bd.y);
+    }
+    // junction: QrivUp[down] += -QrivDown[i], i ascending (MD_f.cpp:236-240)
+    auto up_term = [&](const RivP &qu, double yu0v) {
+        const double ybu = qu.bc > 0 ? m.rybc[qu.bc] : 0.;
+        double yu;
+        const double uu = riv_stage_v<MODE>(yu0v, qu.bc, ybu, &yu);
+        return -riv_down_p(qu, uu, riv_geom_p(qu, yu), ur, q.depth, q.slope);
+    };
+    double qup = 0.;
+    if (nup > 0) qup += up_term(qu0, yu0);
+    if (nup > 1) qup += up_term(qu1, yu1);
+    if (nup > 2) qup += up_term(qu2, yu2);
+    if (nup < 0)
+        for (int k = m.up_off[r], k1 = m.up_off[r + 1]; k < k1; k++) {
+            const int u = m.up_idx[k];
+            qup += up_term(riv_load(p, u), *riv_y_at(Y, u));
+        }
+    // segment sums, ascending reference segment order (MD_f.cpp:228-235)
+    double qsurf = 0., qsub = 0.;
+#pragma unroll
+    for (int j = 0; j < kRivSegBatch; j++)
+        if (j < ns) { qsurf += qv[j].x; qsub += qv[j].y; }
+    for (int k0 = ii.z + kRivSegBatch, k1 = ii.z + ns; k0 < k1; k0 += kRivSegBatch) {   // > 8 segments
+        int pk[kRivSegBatch];
+#pragma unroll
+        for (int j = 0; j < kRivSegBatch; j++) pk[j] = rsort ? k0 + j : m.rseg_pos[k0 + j < k1 ? k0 + j : k0];
+        double2 qk[kRivSegBatch];
+#pragma unroll
+        for (int j = 0; j < kRivSegBatch; j++) qk[j] = p.qseg2[k0 + j < k1 ? pk[j] : pk[0]];
+#pragma unroll
+        for (int j = 0; j < kRivSegBatch; j++)
+            if (k0 + j < k1) { qsurf += qk[j].x; qsub += qk[j].y; }
+    }
+    const double qbc = q.bc < 0 ? qbc0 : 0.0;
+    double dv;
+    if (q.bc > 0) dv = 0.;
+    else if (MODE == 0) {   // MD_f.cpp:162-166
+        dv = (-qup - qsurf - qsub - qdown + qbc) / q.len;
+        if (dv < -1. * g.csarea) dv = -1. * g.csarea;
+        dv = da_to_dy(dv, g.topw, q.bs);                              // fun_dAtodY functions.hpp:125-153
+    } else {                // MD_f_omp.cpp:59
+        dv = (-qup - qsurf - qsub - qdown + qbc) / g.toparea;
+    }
+    dy[3 * Y.n_own + r] = dv;
+    if (DIAG) { dg.qriv_down[r] = qdown; dg.qriv_up[r] = qup; dg.qriv_surf[r] = qsurf; dg.qriv_sub[r] = qsub; }
+}
+#else
 template <int MODE, bool DIAG, int ABL = 0>
 __global__ void __launch_bounds__(256)
 shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, DevDiag dg, int per8) {
@@ -610,6 +733,8 @@ shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     dy[3 * Y.n_own + r] = dv;
     if (DIAG) { dg.qriv_down[r] = qdown; dg.qriv_up[r] = qup; dg.qriv_surf[r] = qsurf; dg.qriv_sub[r] = qsub; }
 }
+
+#endif
 
 void launch_river_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int mode,
                                 bool diag, const DevDiag &dg, hipStream_t s) {

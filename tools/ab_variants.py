@@ -32,6 +32,7 @@ def env_for(v):
     return {"SHUD_RHS_PACKED": "1", "SHUD_RHS_ELE_VARIANT": "0",
             "SHUD_RHS_SEG_ORDER": "reach" if v == "pkR" else "element"}
 res = {v: [] for v in vs}
+rres = {v: [] for v in vs}
 ref = None
 for rnd in range(a.rounds):
     for v in vs:
@@ -47,7 +48,9 @@ for rnd in range(a.rounds):
         same = bool(np.array_equal(out, ref))
         ms, per = h.time_kernels(0.0, dp, dd, a.reps)
         res[v].append(per["shud_ele_kernel"])
+        rres[v].append(per["shud_riv_kernel"])
         print(f"round {rnd} variant {v:5s} {h.layout()}: ele {per['shud_ele_kernel']:.4f} ms riv {per['shud_riv_kernel']:.4f} "
               f"ms  bit-identical={same}", flush=True)
         h.device_free(dp); h.device_free(dd); h.close()
-print(json.dumps({"num_ele": m.num_ele, "ele_ms_median": {v: float(np.median(t)) for v, t in res.items()}}))
+print(json.dumps({"num_ele": m.num_ele, "ele_ms_median": {v: float(np.median(t)) for v, t in res.items()},
+                  "riv_ms_median": {v: float(np.median(t)) for v, t in rres.items()}}))

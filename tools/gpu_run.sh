@@ -5,11 +5,12 @@
 #   suite        pytest -m gpu (full), log + durations        smoke     __graft_entry__.smoke()
 #   bench        the driver's command: bench.py --gpus 1 --steps 20 --warmup 5
 #   quick        RHS-only bench line (no CPU baseline / ET / integrator / e2e)
-#   ab:L1,L2     tools/ab_variants.py on the production lib and each build/ab/libshud_rhs_<L>.so
+#   ab:L1,L2     tools/ab_variants.py (SoA reference + packed, bit-identity checked) on the production lib and each build/ab/libshud_rhs_<L>.so
 #   odeab:L1,L2  integrator ms/step (bench.py integrator section) for the production lib and each A/B lib, twice
 #   kt           rocprofv3 kernel trace of the RHS-only bench            pmc   FETCH_SIZE / WRITE_SIZE passes -> summary
 #   sq           SQ / GRBM counter passes (tools/sq_counters.sh)          ode   integrator kernel trace
 #   part1        bench's N>1 code path on one rank                        rank  tools/rank_timing.py (2/4/8-way)
+#   rankab:L1,L2 tools/rank_timing.py 8 for the production lib and each A/B lib   rankkt  its kernel trace (8-way)
 #   e2e          tools/profile_e2e.sh 1M, 1 day                          redbench  tools/ode_red_bench (reduction forms)
 #   classes      tools/class_sweep.py (element kernel vs #parameter classes, LDS / L2 / SoA)
 #   test:EXPR    pytest -m gpu -k EXPR                                    traj  tests/diag_traj_day.py (ccw one day)
@@ -31,9 +32,9 @@ for step in "$@"; do
     quick) timeout -k 10 300 python bench.py $A --steps 20 --warmup 5 > "$O/quick.json" 2> "$O/quick.err" ;;
     ab:*)
       libs="${step#ab:}"
-      timeout -k 10 300 python tools/ab_variants.py --variants pk --rounds 5 > "$O/ab_prod.log" 2>&1
+      timeout -k 10 300 python tools/ab_variants.py --variants soa0,pk --rounds 5 > "$O/ab_prod.log" 2>&1
       for n in ${libs//,/ }; do
-        SHUD_RHS_LIB=$PWD/shud-up_amd/build/ab/libshud_rhs_$n.so timeout -k 10 300 python tools/ab_variants.py --variants pk --rounds 5 > "$O/ab_$n.log" 2>&1
+        SHUD_RHS_LIB=$PWD/shud-up_amd/build/ab/libshud_rhs_$n.so timeout -k 10 300 python tools/ab_variants.py --variants soa0,pk --rounds 5 > "$O/ab_$n.log" 2>&1
       done
       for f in prod ${libs//,/ }; do echo "$f $(tail -n 1 "$O/ab_$f.log")"; done > "$O/ab_summary.log" ;;
     odeab:*)
@@ -47,6 +48,7 @@ for step in "$@"; do
         done
       done ;;
     kt) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt" -o run -- python3 bench.py $A --steps 20 --warmup 5 > "$O/bench_kt.json" 2> "$O/bench_kt.err" ;;
+    rankkt) timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d "$O/rankkt" -o run -- python3 tools/rank_timing.py 8 > "$O/rankkt.json" 2> "$O/rankkt.err" ;;
     pmc)
       timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch" -o run -- python3 bench.py $A --steps 5 --warmup 1 > "$O/pmc_fetch.log" 2>&1
       timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_write" -o run -- python3 bench.py $A --steps 5 --warmup 1 > "$O/pmc_write.log" 2>&1
@@ -55,6 +57,12 @@ for step in "$@"; do
     ode) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt_ode" -o run -- python3 bench.py --no-cpu-baseline --no-et --no-many-class --no-host-vectors --e2e-ele 0 --steps 5 --warmup 1 > "$O/bench_ode_kt.json" 2> "$O/bench_ode_kt.err" ;;
     part1) timeout -k 10 300 python bench.py $A --partition-1 --steps 20 > "$O/bench_partition1.json" 2> "$O/bench_partition1.err" ;;
     rank) timeout -k 10 400 python tools/rank_timing.py > "$O/rank_timing.json" 2> "$O/rank_timing.err" ;;
+    rankab:*)                   # rankab:L1,L2 -> 8-way rank timing for the production lib and each A/B lib
+      libs="${step#rankab:}"
+      for n in prod ${libs//,/ }; do
+        if [ $n = prod ]; then L=""; else L=$PWD/shud-up_amd/build/ab/libshud_rhs_$n.so; fi
+        SHUD_RHS_LIB=$L timeout -k 10 300 python tools/rank_timing.py 8 > "$O/rank8_$n.json" 2> "$O/rank8_$n.err"
+      done ;;
     e2e) timeout -k 10 600 bash tools/profile_e2e.sh 1000000 1 > "$O/e2e.log" 2>&1 ;;
     traj) timeout -k 10 300 python tests/diag_traj_day.py "$O/traj_ccw_day.json" > "$O/traj_ccw_day.log" 2>&1 ;;
     classes) timeout -k 10 600 python tools/class_sweep.py > "$O/class_sweep.log" 2>&1 ;;
