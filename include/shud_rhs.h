@@ -54,6 +54,8 @@ extern "C" {
 /* ET-step prelude (include/shud_et.h, shud_et_step) */
 #define SHUD_EF_ET_RA        0x20u  /* CheckNonZero(Aerodynamic Resistance) MD_ET.cpp:273     [10] */
 #define SHUD_EF_ET_PT_NAN    0x40u  /* CheckNANi(qPotTran)          MD_ET.cpp:278              [10] */
+/* partitioned handles */
+#define SHUD_EF_HALO_WAIT    0x80u  /* boundary elements timed out waiting for the halo exchange (no reference analogue) */
 
 /* Static mesh description (uploaded once by shud_rhs_create).  Mirrors the derived geometry the
  * reference holds after Model_Data::initialize() (MD_initialize.cpp:168-245). */

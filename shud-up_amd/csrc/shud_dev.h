@@ -170,6 +170,16 @@ void launch_element_kernel(const DevMesh &m, const YView &Y, double *dy, int n_c
 void launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1,
                                   int cur, int mode, bool open, bool diag, bool fu_unit, const DevDiag &dg,
                                   hipStream_t s, const DevLake *lake = nullptr, bool interior = false);
+// partitioned handles: the boundary + ghost elements [n_int, n_all) ride at the end of the interior element launch;
+// their workgroups wait until the comm stream has published the halo (flag >= epoch; epoch 0 = stream-ordered)
+struct HaloWait {
+    const unsigned long long *flag;
+    unsigned long long epoch;
+};
+bool launch_element_kernel_packed_fold(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int n_int,
+                                       int n_all, int cur, int mode, bool open, bool fu_unit, const DevDiag &dg,
+                                       const HaloWait &hw, hipStream_t s);
+void launch_halo_flag(unsigned long long *flag, unsigned long long epoch, hipStream_t s);
 void launch_river_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int mode,
                                 bool diag, const DevDiag &dg, hipStream_t s);
 void launch_lake_kernel(const DevMesh &m, const DevPacked &p, const DevLake &L, const YView &Y, double *dy,

@@ -194,6 +194,60 @@ shud_ele_kernel_packed_big(DevMesh m, DevPacked p, YView Y, double *__restrict__
     if (act) ele_body<MODE, OPEN, DIAG, FU1, true, false, GH>(m, p, Y, dy, i, cur, dg, lk, lct, own);
 }
 
+// Partitioned handles: one launch for the interior elements [0, n_int) (ghost-free instantiation, XCD-chunked
+// tiles, blocks [0, nb_int)) and, in the blocks after them, the boundary + ghost elements [n_int, n_all), which read
+// halo data.  A boundary workgroup is dispatched after every interior one, so by then the halo exchange on the comm
+// stream has normally long finished; each of its waves still checks the comm stream's flag (one lane polls, agent
+// scope) and takes an agent-scope acquire before its first halo read.  The comm stream's work never waits for this
+// kernel (the flag is enqueued before it), so the poll always ends; it is bounded anyway (SHUD_EF_HALO_WAIT).
+// Saves the boundary launch (a lone generation of a few workgroups, ~12 us at 8 ranks) and its cross-queue wait.
+constexpr int kHaloPollMax = 1 << 22;                   // x s_sleep(8) ~ 2^31 cycles ~ 1 s
+__device__ __forceinline__ void halo_wait(const DevMesh &m, const HaloWait &hw, int i) {
+    if (hw.epoch == 0) return;
+    bool late = false;
+    if (__lane_id() == 0) {
+        int n = 0;
+        while (__hip_atomic_load(hw.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < hw.epoch) {
+            __builtin_amdgcn_s_sleep(8);
+            if (++n >= kHaloPollMax) { late = true; break; }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    report_w(m.err, late, 0x80u, 7, i);                      // SHUD_EF_HALO_WAIT
+}
+template <int MODE, bool OPEN, bool FU1>
+__global__ void __launch_bounds__(256, SHUD_ELE_WAVES)
+shud_ele_kernel_packed_fold(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int n_int, int n_all, int cur,
+                            DevDiag dg, int per8, int nb_int, HaloWait hw) {
+    extern __shared__ double lct[];
+    const DevLake lk{};
+    if ((int)blockIdx.x < nb_int) {
+        const int i = tile_of(per8) * 256 + (int)threadIdx.x;
+        const bool act = i < n_int;
+        double tv[kTabBatch];
+        tab_issue<256>(p, tv);
+        OwnRec own;
+        if (act) own = load_own<FU1, false>(p, Y, i, cur);
+        tab_store<256>(p, tv, lct);
+        __syncthreads();
+        if (act) ele_body<MODE, OPEN, false, FU1, true, false, false>(m, p, Y, dy, i, cur, dg, lk, lct, own);
+        return;
+    }
+    const int i = n_int + ((int)blockIdx.x - nb_int) * 256 + (int)threadIdx.x;
+    const bool act = i < n_all;
+    double tv[kTabBatch];
+    tab_issue<256>(p, tv);
+    halo_wait(m, hw, act ? i : n_int);
+    OwnRec own;
+    if (act) own = load_own<FU1, true>(p, Y, i, cur);
+    tab_store<256>(p, tv, lct);
+    __syncthreads();
+    if (act) ele_body<MODE, OPEN, false, FU1, true, false, true>(m, p, Y, dy, i, cur, dg, lk, lct, own);
+}
+__global__ void shud_halo_flag_kernel(unsigned long long *flag, unsigned long long epoch) {
+    if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
 __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, const YView &Y, double *__restrict__ dy,
                                          int i, int cur, const DevDiag &dg, const DevLake &lk, const double *lct,
@@ -913,6 +967,29 @@ void launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YV
 #undef LDI
 #undef LFU
 #undef LP
+}
+
+// false: this configuration has no folded instantiation (the caller launches interior and boundary separately)
+bool launch_element_kernel_packed_fold(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int n_int,
+                                       int n_all, int cur, int mode, bool open, bool fu_unit, const DevDiag &dg,
+                                       const HaloWait &hw, hipStream_t s) {
+    if (n_int <= 0 || n_all <= n_int || p.ncls > LDS_CLS_MAX) return false;
+    const int nb_int = ((n_int + 255) / 256 + 7) / 8 * 8, nb_b = (n_all - n_int + 255) / 256;
+    const size_t lds = (size_t)p.ncls * CF_LDS_STRIDE * sizeof(double);
+#define LF(MO, OP, FU) hipLaunchKernelGGL((shud_ele_kernel_packed_fold<MO, OP, FU>), dim3(nb_int + nb_b), dim3(256), lds, \
+                                          s, m, p, Y, dy, n_int, n_all, cur, dg, nb_int / 8, nb_int, hw)
+    if (mode == 0) {
+        if (open) { if (fu_unit) LF(0, true, true); else LF(0, true, false); }
+        else { if (fu_unit) LF(0, false, true); else LF(0, false, false); }
+    } else {
+        if (open) { if (fu_unit) LF(1, true, true); else LF(1, true, false); }
+        else { if (fu_unit) LF(1, false, true); else LF(1, false, false); }
+    }
+#undef LF
+    return true;
+}
+void launch_halo_flag(unsigned long long *flag, unsigned long long epoch, hipStream_t s) {
+    hipLaunchKernelGGL(shud_halo_flag_kernel, dim3(1), dim3(64), 0, s, flag, epoch);
 }
 
 void launch_pack_step_kernel(const DevMesh &m, const DevPacked &p, int n, int cur, unsigned what, hipStream_t s) {

@@ -89,6 +89,10 @@ struct shud_rhs {
     ncclComm_t comm = nullptr;
     hipStream_t s_comm = nullptr;        // RCCL halo exchange, overlapped with the interior element kernel
     hipEvent_t ev_pack = nullptr, ev_comm = nullptr;
+    // boundary + ghost elements folded into the interior launch (launch_element_kernel_packed_fold): the comm stream
+    // publishes halo_epoch into d_halo_flag after the exchange; SHUD_RHS_FOLD=0 keeps two launches (A/B)
+    bool fold = false;
+    unsigned long long *d_halo_flag = nullptr, halo_epoch = 0;
     // in-loop kernel timing (shud_rhs_timing): 3 events per device eval {start, after element kernel(s),
     // after river (+lake) kernel}, recorded on the handle's stream while enabled
     int tm_cap = 0, tm_n = 0, tm_stride = 1;

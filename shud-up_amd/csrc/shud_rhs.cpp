@@ -660,6 +660,9 @@ static int setup_partition(shud_rhs *h, const ShudPartition *part) {
     HIP_TRY(hipStreamCreateWithFlags(&h->s_comm, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&h->ev_pack, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&h->ev_comm, hipEventDisableTiming));
+    if ((rc = h->upload(&h->d_halo_flag, (const unsigned long long *)nullptr, 1))) return rc;
+    const char *fe = getenv("SHUD_RHS_FOLD");
+    h->fold = !(fe && fe[0] == '0');
     return 0;
 }
 
@@ -790,6 +793,7 @@ static int exchange(shud_rhs *h, const double *y) {
     }
     NCCL_TRY(ncclGroupEnd());
     }                                // external transport (tests): the caller placed the ghost buffers
+    if (h->fold) launch_halo_flag(h->d_halo_flag, ++h->halo_epoch, h->s_comm);
     HIP_TRY(hipEventRecord(h->ev_comm, h->s_comm));
     return 0;
 }
@@ -839,7 +843,7 @@ int shud_read_err(shud_rhs *h) {
 }
 static int read_err(shud_rhs *h) { return shud_read_err(h); }
 
-static const uint32_t kFatal = SHUD_EF_NAN_QELE | SHUD_EF_EFFKH | SHUD_EF_ET_NEG | SHUD_EF_ET_NAN;
+static const uint32_t kFatal = SHUD_EF_NAN_QELE | SHUD_EF_EFFKH | SHUD_EF_ET_NEG | SHUD_EF_ET_NAN | SHUD_EF_HALO_WAIT;
 
 // partitioned handles: the interior elements [0, n_int) run while the halo exchange is in flight (RCCL on
 // s_comm); boundary + ghost elements and the reaches wait for it.  Unpartitioned: one launch each.
@@ -847,7 +851,22 @@ static const uint32_t kFatal = SHUD_EF_NAN_QELE | SHUD_EF_EFFKH | SHUD_EF_ET_NEG
 #ifndef SHUD_ABL_NOSPLIT
 #define SHUD_ABL_NOSPLIT 0
 #endif
-static int launch_split(shud_rhs *h, const double *y, double *dy, hipEvent_t e_mid = nullptr) {
+// stream_halo: the halo is already ordered on the main stream (eval_compute, external transport) — the folded
+// launch's boundary workgroups then skip the flag
+static int launch_split(shud_rhs *h, const double *y, double *dy, hipEvent_t e_mid = nullptr,
+                        bool stream_halo = false) {
+    if (h->fold && h->packed && !h->variant && !h->lakeon && !SHUD_ABL_NOSPLIT) {
+        YView Y{y, h->d_gele, h->d_griv, h->n_own, h->n_own_riv};
+        const HaloWait hw{h->d_halo_flag, stream_halo ? 0ull : h->halo_epoch};
+        if (launch_element_kernel_packed_fold(h->dm, h->dp, Y, dy, h->n_int, h->n_own + h->n_segghost, h->cur,
+                                              h->mode, h->open, h->fu_unit[0] && h->fu_unit[1], h->dd, hw,
+                                              h->stream)) {
+            if (e_mid) HIP_TRY(hipEventRecord(e_mid, h->stream));
+            launch_riv(h, y, dy, false);             // after the boundary workgroups, which saw the halo
+            HIP_TRY(hipGetLastError());
+            return 0;
+        }
+    }
     if (h->partitioned && h->packed && !h->variant && h->n_int > 0 && !SHUD_ABL_NOSPLIT) {
         launch_ele(h, y, dy, h->cur, h->cur_e, false, 0, h->n_int);
         HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_comm, 0));
@@ -1112,7 +1131,7 @@ extern "C" int shud_rhs_eval_compute(shud_rhs_t h, double t, const double *d_y, 
     if (!h) return shud_fail(SHUD_ERR_ARG, "null argument");
     h->last_cur = h->cur;
     h->last_cur_e = h->cur_e;
-    int rc = launch_split(h, d_y, d_ydot);
+    int rc = launch_split(h, d_y, d_ydot, nullptr, true);
     if (rc) return rc;
     flip(h);
     h->last_y = d_y;
