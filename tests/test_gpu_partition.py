@@ -17,7 +17,7 @@ from shud_rhs import partition, workload
 pytestmark = pytest.mark.gpu
 
 
-def _run_ranks(m, y_list, locs, mode, ncalls=3):
+def _run_ranks(m, y_list, locs, mode, ncalls=3, device_eval=False):
     """locs: [(local ShudModel, LocalPartition)] for every rank; compares owned DY with one unpartitioned
     handle over `ncalls` successive stateful calls per state."""
     from shud_rhs import runtime as rt
@@ -63,8 +63,13 @@ def _run_ranks(m, y_list, locs, mode, ncalls=3):
                             rt.lib().shud_rhs_memcpy(hs[r].h, C.c_void_p(griv + 8 * d0), C.c_void_p(rsend + 8 * s0),
                                                      8 * (s1 - s0), 3)
                 for r, (lm, part) in enumerate(locs):
-                    hs[r].eval_compute(0.0, bufs[r][0], bufs[r][1])
+                    if device_eval:     # the full device eval: pack + halo flag on the comm stream, folded launch
+                        hs[r].eval_device(0.0, bufs[r][0], bufs[r][1])
+                    else:
+                        hs[r].eval_compute(0.0, bufs[r][0], bufs[r][1])
                     got = hs[r].d2h(np.zeros(bufs[r][2]), bufs[r][1])
+                    if device_eval:
+                        assert hs[r].get_error()["flags"] & 0x80 == 0, "SHUD_EF_HALO_WAIT"
                     want = partition.local_state(ref, m, part)
                     assert np.array_equal(got, want, equal_nan=True), f"rank {r} call {call}: {(got != want).sum()} differ"
     finally:
@@ -85,6 +90,19 @@ def test_partitioned_handles_bit_identical(nranks, mode, packed, monkeypatch):
     _, _, plans = partition.build_plans(m, nranks)
     locs = [partition.local_model(m, plans[r], r, nranks) for r in range(nranks)]
     _run_ranks(m, [y, workload.random_state(m, seed=2)], locs, mode)
+
+
+@pytest.mark.parametrize("fold", ["1", "0"])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_device_eval_halo_flag(fold, mode, monkeypatch):
+    """shud_rhs_eval on partitioned handles (external transport, halo placed by the test): the comm stream packs
+    and publishes the halo epoch; with SHUD_RHS_FOLD=1 the boundary + ghost elements run in the interior launch and
+    poll that flag, with 0 they are a second launch behind the comm event.  Both bit-identical to one GPU."""
+    monkeypatch.setenv("SHUD_RHS_FOLD", fold)
+    m, y = cases.variant(20000, seed=23)
+    ep, _ = partition.cpp_partition(m, 4, partition.PART_AUTO)
+    locs = [partition.CppPlan(m, ep, 4, r).local_model() for r in range(4)]
+    _run_ranks(m, [y, workload.random_state(m, seed=8)], locs, mode, ncalls=2, device_eval=True)
 
 
 @pytest.mark.parametrize("nranks", [2, 4, 8])

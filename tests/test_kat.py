@@ -110,7 +110,8 @@ def py_dady(dA, w, s):                      # functions.hpp:125-153
     if dA == 0.:
         return 0.
     if abs(s) < EPS_SLOPE:
-        return dA / w
+        with np.errstate(divide="ignore", invalid="ignore"):   # w = 0 is a KAT case: IEEE inf/NaN as in C
+            return dA / w
     s = abs(s)
     cc = w * w + 4 * s * dA
     return -1. * w / (2. * s) if cc < ZERO else (-w + math.sqrt(cc)) / (2 * s)
