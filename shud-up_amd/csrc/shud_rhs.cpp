@@ -32,6 +32,17 @@ namespace {
 thread_local std::string g_last_error;
 }  // namespace
 
+// Event scopes.  Every event here orders work between queues of one device (the comm stream's pack / exchange and
+// the main stream's kernels) or times kernels: a device-scope release is enough for both, and the default
+// system-scope release writes the L2's dirty lines back to HBM at every record (SHUD_EV_SCOPE=0: the HIP
+// defaults, A/B only).  RCCL's own kernels on s_comm complete before ev_comm, which then publishes their writes
+// to this device's other queues.
+#ifndef SHUD_EV_SCOPE
+#define SHUD_EV_SCOPE 1
+#endif
+static constexpr unsigned kEvSync = SHUD_EV_SCOPE ? hipEventDisableSystemFence : 0u;
+static constexpr unsigned kEvTime = SHUD_EV_SCOPE ? hipEventReleaseToDevice : hipEventDefault;
+
 int shud_fail(int code, const char *fmt, ...) {
     char buf[512];
     va_list ap;
@@ -658,8 +669,8 @@ static int setup_partition(shud_rhs *h, const ShudPartition *part) {
     // the pack kernel and the exchange run on a side stream beside the interior element kernel (RCCL and
     // external transport alike, so the one-GPU rank timings measure the same pipeline)
     HIP_TRY(hipStreamCreateWithFlags(&h->s_comm, hipStreamNonBlocking));
-    HIP_TRY(hipEventCreateWithFlags(&h->ev_pack, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&h->ev_comm, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&h->ev_pack, hipEventDisableTiming | kEvSync));
+    HIP_TRY(hipEventCreateWithFlags(&h->ev_comm, hipEventDisableTiming | kEvSync));
     if ((rc = h->upload(&h->d_halo_flag, (const unsigned long long *)nullptr, 1))) return rc;
     const char *fe = getenv("SHUD_RHS_FOLD");
     h->fold = !(fe && fe[0] == '0');
@@ -1147,7 +1158,7 @@ extern "C" int shud_rhs_timing(shud_rhs_t h, int max_evals, int stride) {
     const size_t need = 3 * (size_t)max_evals;
     while (h->tm_ev.size() < need) {
         hipEvent_t e;
-        HIP_TRY(hipEventCreate(&e));
+        HIP_TRY(hipEventCreateWithFlags(&e, kEvTime));
         h->tm_ev.push_back(e);
     }
     h->tm_cap = max_evals;
@@ -1187,7 +1198,7 @@ extern "C" int shud_rhs_time_kernels(shud_rhs_t h, double t, const double *d_y, 
     HIP_TRY(hipSetDevice(h->device));
     const int K = h->partitioned ? 3 : 2;
     std::vector<hipEvent_t> ev((size_t)reps * (K + 1));
-    for (auto &e : ev) HIP_TRY(hipEventCreate(&e));
+    for (auto &e : ev) HIP_TRY(hipEventCreateWithFlags(&e, kEvTime));
     for (int r = 0; r < reps; r++) {
         hipEvent_t *E = &ev[(size_t)r * (K + 1)];
         int k = 0;

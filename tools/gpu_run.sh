@@ -5,6 +5,7 @@
 #   suite        pytest -m gpu (full), log + durations        smoke     __graft_entry__.smoke()
 #   bench        the driver's command: bench.py --gpus 1 --steps 20 --warmup 5
 #   quick        RHS-only bench line (no CPU baseline / ET / integrator / e2e)
+#   quickab:L1,L2  the RHS-only bench line for the production lib and each A/B lib, twice
 #   ab:L1,L2     tools/ab_variants.py (SoA reference + packed, bit-identity checked) on the production lib and each build/ab/libshud_rhs_<L>.so
 #   odeab:L1,L2  integrator ms/step (bench.py integrator section) for the production lib and each A/B lib, twice
 #   kt           rocprofv3 kernel trace of the RHS-only bench            pmc   FETCH_SIZE / WRITE_SIZE passes -> summary
@@ -31,6 +32,15 @@ for step in "$@"; do
     smoke) timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 ;;
     bench) timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > "$O/bench.json" 2> "$O/bench.err" ;;
     quick) timeout -k 10 300 python bench.py $A --steps 20 --warmup 5 > "$O/quick.json" 2> "$O/quick.err" ;;
+    quickab:*)                  # quickab:L1,L2 -> RHS-only bench line for the production lib and each A/B lib, 2 rounds
+      libs="${step#quickab:}"
+      for rep in 1 2; do
+        for n in prod ${libs//,/ }; do
+          if [ $n = prod ]; then L=""; else L=$PWD/shud-up_amd/build/ab/libshud_rhs_$n.so; fi
+          SHUD_RHS_LIB=$L timeout -k 10 300 python bench.py $A --steps 40 --warmup 5 > "$O/quick_${n}_$rep.json" 2> "$O/quick_${n}_$rep.err"
+          echo "$n rep$rep $(python -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['ms_per_step'], d['roofline']['kernel_ms'])" "$O/quick_${n}_$rep.json")" >> "$O/quickab_summary.log"
+        done
+      done ;;
     ab:*)
       libs="${step#ab:}"
       timeout -k 10 300 python tools/ab_variants.py --variants soa0,pk --rounds 5 > "$O/ab_prod.log" 2>&1
