@@ -1,16 +1,20 @@
 """A/B the element-kernel build variants on one mesh in one process (interleaved, n rounds).
 Every variant must produce bit-identical ydot (same arithmetic, different schedule/placement).
-usage: python tools/ab_variants.py [--n-ele N] [--variants 0,1,2,...] [--rounds 3] [--reps 20]"""
+usage: python tools/ab_variants.py [--n-ele N] [--variants 0,1,2,...] [--rounds 3] [--reps 20]
+A variant lib:NAME runs the packed kernel of shud-up_amd/build/ab/libshud_rhs_NAME.so (tools/ablib.sh), loaded
+beside the production library in the same process, so library builds interleave round by round."""
 import argparse
 import json
 import os
 import sys
 
+import ctypes as C
+
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "shud-up_amd"))
-from shud_rhs import runtime, synth, workload  # noqa: E402
+from shud_rhs import abi, runtime, synth, workload  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--n-ele", type=int, default=10_000_000)
@@ -26,7 +30,21 @@ y = workload.random_state(m)
 vs = a.variants.split(",")
 
 
+_libs = {}
+
+
+def lib_for(v):
+    """the bound library a variant runs on: production, or an A/B build loaded RTLD_LOCAL beside it"""
+    if not v.startswith("lib:"):
+        return runtime.lib() if "prod" not in _libs else _libs["prod"]
+    if v not in _libs:
+        _libs[v] = abi.bind(C.CDLL(os.path.join(ROOT, "shud-up_amd", "build", "ab", f"libshud_rhs_{v[4:]}.so")))
+    return _libs[v]
+
+
 def env_for(v):
+    if v.startswith("lib:"):
+        return {"SHUD_RHS_PACKED": "1", "SHUD_RHS_ELE_VARIANT": "0", "SHUD_RHS_SEG_ORDER": "element"}
     if v.startswith("soa"):
         return {"SHUD_RHS_PACKED": "0", "SHUD_RHS_ELE_VARIANT": v[3:] or "0"}
     return {"SHUD_RHS_PACKED": "1", "SHUD_RHS_ELE_VARIANT": "0",
@@ -34,9 +52,11 @@ def env_for(v):
 res = {v: [] for v in vs}
 rres = {v: [] for v in vs}
 ref = None
+_libs["prod"] = runtime.lib()
 for rnd in range(a.rounds):
     for v in vs:
         os.environ.update(env_for(v))
+        runtime._LIB = lib_for(v)                 # every call of this handle goes to the variant's library
         h = runtime.RhsHandle(m)
         h.set_step_inputs()
         dp, dd = h.device_alloc(8 * m.num_y), h.device_alloc(8 * m.num_y)
@@ -52,5 +72,6 @@ for rnd in range(a.rounds):
         print(f"round {rnd} variant {v:5s} {h.layout()}: ele {per['shud_ele_kernel']:.4f} ms riv {per['shud_riv_kernel']:.4f} "
               f"ms  bit-identical={same}", flush=True)
         h.device_free(dp); h.device_free(dd); h.close()
+        runtime._LIB = _libs["prod"]
 print(json.dumps({"num_ele": m.num_ele, "ele_ms_median": {v: float(np.median(t)) for v, t in res.items()},
                   "riv_ms_median": {v: float(np.median(t)) for v, t in rres.items()}}))

@@ -6,6 +6,7 @@
 #   bench        the driver's command: bench.py --gpus 1 --steps 20 --warmup 5
 #   quick        RHS-only bench line (no CPU baseline / ET / integrator / e2e)
 #   quickab:L1,L2  the RHS-only bench line for the production lib and each A/B lib, twice
+#   abl:L1,L2    tools/ab_variants.py, production + each A/B lib loaded side by side, interleaved per round
 #   ab:L1,L2     tools/ab_variants.py (SoA reference + packed, bit-identity checked) on the production lib and each build/ab/libshud_rhs_<L>.so
 #   odeab:L1,L2  integrator ms/step (bench.py integrator section) for the production lib and each A/B lib, twice
 #   kt           rocprofv3 kernel trace of the RHS-only bench            pmc   FETCH_SIZE / WRITE_SIZE passes -> summary
@@ -41,6 +42,11 @@ for step in "$@"; do
           echo "$n rep$rep $(python -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['ms_per_step'], d['roofline']['kernel_ms'])" "$O/quick_${n}_$rep.json")" >> "$O/quickab_summary.log"
         done
       done ;;
+    abl:*)                      # abl:L1,L2 -> production packed kernel and each A/B lib interleaved in one process, 9 rounds
+      libs="${step#abl:}"; vs="pk"
+      for n in ${libs//,/ }; do vs="$vs,lib:$n"; done
+      timeout -k 10 400 python tools/ab_variants.py --variants $vs --rounds 9 > "$O/abl.log" 2>&1
+      tail -n 1 "$O/abl.log" > "$O/abl_summary.log" ;;
     ab:*)
       libs="${step#ab:}"
       timeout -k 10 300 python tools/ab_variants.py --variants soa0,pk --rounds 5 > "$O/ab_prod.log" 2>&1
