@@ -6,6 +6,7 @@
 #   bench        the driver's command: bench.py --gpus 1 --steps 20 --warmup 5
 #   quick        RHS-only bench line (no CPU baseline / ET / integrator / e2e)
 #   quickab:L1,L2  the RHS-only bench line for the production lib and each A/B lib, twice
+#   abv:V1,V2    tools/ab_variants.py --variants V1,V2 (e.g. pk,pkR) on the production lib, 9 rounds
 #   abl:L1,L2    tools/ab_variants.py, production + each A/B lib loaded side by side, interleaved per round
 #   ab:L1,L2     tools/ab_variants.py (SoA reference + packed, bit-identity checked) on the production lib and each build/ab/libshud_rhs_<L>.so
 #   odeab:L1,L2  integrator ms/step (bench.py integrator section) for the production lib and each A/B lib, twice
@@ -42,6 +43,9 @@ for step in "$@"; do
           echo "$n rep$rep $(python -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['ms_per_step'], d['roofline']['kernel_ms'])" "$O/quick_${n}_$rep.json")" >> "$O/quickab_summary.log"
         done
       done ;;
+    abv:*)                      # abv:V1,V2 -> tools/ab_variants.py on the production lib with these variants, 9 rounds
+      timeout -k 10 400 python tools/ab_variants.py --variants "${step#abv:}" --rounds 9 > "$O/abv.log" 2>&1
+      tail -n 1 "$O/abv.log" > "$O/abv_summary.log" ;;
     abl:*)                      # abl:L1,L2 -> production packed kernel and each A/B lib interleaved in one process, 9 rounds
       libs="${step#abl:}"; vs="pk"
       for n in ${libs//,/ }; do vs="$vs,lib:$n"; done
