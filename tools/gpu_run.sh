@@ -11,6 +11,7 @@
 #   ab:L1,L2     tools/ab_variants.py (SoA reference + packed, bit-identity checked) on the production lib and each build/ab/libshud_rhs_<L>.so
 #   odeab:L1,L2  integrator ms/step (bench.py integrator section) for the production lib and each A/B lib, twice
 #   kt           rocprofv3 kernel trace of the RHS-only bench            pmc   FETCH_SIZE / WRITE_SIZE passes -> summary
+#   calib        PMC calibration kernels (tools/calibrate_pmc)                tcc   L2 hit/miss of the RHS kernels
 #   sq           SQ / GRBM counter passes (tools/sq_counters.sh)          ode   integrator kernel trace
 #   part1        bench's N>1 code path on one rank                        rank  tools/rank_timing.py (2/4/8-way)
 #   rankab:L1,L2 tools/rank_timing.py 8 for the production lib and each A/B lib   rankkt  its kernel trace (8-way)
@@ -77,6 +78,14 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch" -o run -- python3 bench.py $A --steps 5 --warmup 1 > "$O/pmc_fetch.log" 2>&1
       timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_write" -o run -- python3 bench.py $A --steps 5 --warmup 1 > "$O/pmc_write.log" 2>&1
       python3 tools/pmc_summary.py "$O/pmc_fetch" "$O/pmc_write" 10001406 "$O/pmc_summary.json" > /dev/null ;;
+    calib)                      # FETCH_SIZE / WRITE_SIZE of the known-byte kernels (tools/calibrate_pmc, built in-tree)
+      timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/calib_fetch" -o run -- ./tools/calibrate_pmc > "$O/calib_fetch.log" 2>&1
+      timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/calib_write" -o run -- ./tools/calibrate_pmc > "$O/calib_write.log" 2>&1
+      python3 tools/pmc_counters.py "$O/calib_fetch" > "$O/calib_summary.txt"
+      python3 tools/pmc_counters.py "$O/calib_write" >> "$O/calib_summary.txt" ;;
+    tcc)                        # L2 hit / miss of the RHS kernels (RHS-only bench)
+      timeout -k 10 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$O/tcc" -o run -- python3 bench.py $A --steps 5 --warmup 1 > "$O/tcc.log" 2>&1
+      python3 tools/pmc_counters.py "$O/tcc" ele_kernel riv_kernel > "$O/tcc_summary.txt" ;;
     sq) timeout -k 10 400 bash tools/sq_counters.sh "$O" > /dev/null ;;
     ode) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt_ode" -o run -- python3 bench.py --no-cpu-baseline --no-et --no-many-class --no-host-vectors --e2e-ele 0 --steps 5 --warmup 1 > "$O/bench_ode_kt.json" 2> "$O/bench_ode_kt.err" ;;
     part1) timeout -k 10 300 python bench.py $A --partition-1 --steps 20 > "$O/bench_partition1.json" 2> "$O/bench_partition1.err" ;;
