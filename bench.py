@@ -449,9 +449,14 @@ def pmc_traffic(NE):
     k = pj.get("kernels", {})
     if "shud_ele_kernel" in k:
         out["traffic"] = k["shud_ele_kernel"]["hbm_bytes_per_launch"]
-        out["traffic_source"] = "profiles/pmc_summary.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE; corrected)"
+        out["traffic_source"] = ("profiles/pmc_summary.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE; per-pattern "
+                                 "gfx950 calibration, profiles/r03/pmc_calib/)")
+        if "hbm_bytes_blanket_x2" in k["shud_ele_kernel"]:
+            out["traffic_blanket_x2"] = k["shud_ele_kernel"]["hbm_bytes_blanket_x2"]
     if "shud_riv_kernel" in k:
         out["riv_traffic"] = k["shud_riv_kernel"]["hbm_bytes_per_launch"]
+        if "hbm_bytes_blanket_x2" in k["shud_riv_kernel"]:
+            out["riv_traffic_blanket_x2"] = k["shud_riv_kernel"]["hbm_bytes_blanket_x2"]
     return out
 
 

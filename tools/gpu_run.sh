@@ -77,7 +77,7 @@ for step in "$@"; do
     pmc)
       timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch" -o run -- python3 bench.py $A --steps 5 --warmup 1 > "$O/pmc_fetch.log" 2>&1
       timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_write" -o run -- python3 bench.py $A --steps 5 --warmup 1 > "$O/pmc_write.log" 2>&1
-      python3 tools/pmc_summary.py "$O/pmc_fetch" "$O/pmc_write" 10001406 "$O/pmc_summary.json" > /dev/null ;;
+      python3 tools/pmc_summary.py "$O/pmc_fetch" "$O/pmc_write" 10001406 "$O/pmc_summary.json" 972842 5003338 > /dev/null ;;
     calib)                      # FETCH_SIZE / WRITE_SIZE of the known-byte kernels (tools/calibrate_pmc, built in-tree)
       timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/calib_fetch" -o run -- ./tools/calibrate_pmc > "$O/calib_fetch.log" 2>&1
       timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/calib_write" -o run -- ./tools/calibrate_pmc > "$O/calib_write.log" 2>&1
