@@ -16,6 +16,7 @@
 #   part1        bench's N>1 code path on one rank                        rank  tools/rank_timing.py (2/4/8-way)
 #   rankab:L1,L2 tools/rank_timing.py 8 for the production lib and each A/B lib   rankkt  its kernel trace (8-way)
 #   rankfold     8-way rank timing, boundary elements folded into the interior launch vs split (SHUD_RHS_FOLD=0)
+#   syn1m        tools/profile_1m.sh (BASELINE configs[3]: bench line, kernel trace, PMC)   sizes  RHS lines at 1.25/2.5/5M + OMP
 #   e2e          tools/profile_e2e.sh 1M, 1 day                          redbench  tools/ode_red_bench (reduction forms)
 #   classes      tools/class_sweep.py (element kernel vs #parameter classes, LDS / L2 / SoA)
 #   test:EXPR    pytest -m gpu -k EXPR                                    traj  tests/diag_traj_day.py (ccw one day)
@@ -96,6 +97,12 @@ for step in "$@"; do
         if [ $n = prod ]; then L=""; else L=$PWD/shud-up_amd/build/ab/libshud_rhs_$n.so; fi
         SHUD_RHS_LIB=$L timeout -k 10 300 python tools/rank_timing.py 8 > "$O/rank8_$n.json" 2> "$O/rank8_$n.err"
       done ;;
+    syn1m) timeout -k 10 900 bash tools/profile_1m.sh "$O/syn1M" > "$O/syn1M.log" 2>&1 ;;
+    sizes)                      # RHS-only bench lines at other mesh sizes and in OMP semantics
+      for n in 1250000 2500000 5000000; do
+        timeout -k 10 300 python bench.py $A --n-ele $n --steps 100 --warmup 10 > "$O/rhs_$n.json" 2> "$O/rhs_$n.err"
+      done
+      timeout -k 10 300 python bench.py $A --mode omp --steps 40 --warmup 5 > "$O/rhs_omp.json" 2> "$O/rhs_omp.err" ;;
     e2e) timeout -k 10 600 bash tools/profile_e2e.sh 1000000 1 > "$O/e2e.log" 2>&1 ;;
     traj) timeout -k 10 300 python tests/diag_traj_day.py "$O/traj_ccw_day.json" > "$O/traj_ccw_day.log" 2>&1 ;;
     classes) timeout -k 10 600 python tools/class_sweep.py > "$O/class_sweep.log" 2>&1 ;;
