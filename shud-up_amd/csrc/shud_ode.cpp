@@ -88,6 +88,9 @@ struct shud_ode {
     double rl1 = 0, gamma = 0, gammap = 0, gamrat = 1, crate = 1, delp = 0, acnrm = 0, saved_tq5 = 0;
     double tstop = 0, tretlast = 0, tolsf = 1, etaq = 0, etaqm1 = 0, etaqp1 = 0, nrmfac = 1;
     bool acor_zero = false;
+    // acor_lazy: acor is logically all +0.0 but was never stored (the last predict skipped the fill,
+    // ode::lazy_ycor()); cleared by the first newton_update, which writes all of acor
+    bool acor_lazy = false;
     int tstopset = 0, q = 1, qprime = 1, next_q = 1, qwait = 2, L = 2, qu = 0, indx_acor = 5;
     int convfail = 0, jcur = 0, jbad = 0, curiter = 0, initialized = 0;
     int64_t nst = 0, nscon = 0, nstlp = 0, nfe = 0, nfeDQ = 0, nni = 0, nnf = 0, ncfn = 0, netf = 0, nsetups = 0;
@@ -183,19 +186,21 @@ struct shud_ode {
         gamrat = (nst > 0) ? gamma / gammap : 1.0;
     }
     // ---- cvPredict / cvRestore / cvRescale ----
-    // y_pred: the last predict also wrote y = zn[0] + 0 and acor = 0 (k_pascal), which the cvNls start that
-    // always follows it would otherwise do in a separate pass (k_vsum_zero)
+    // y_pred: the last predict also wrote y = zn[0] + 0 and set acor = 0 (k_pascal; with lazy_ycor the zeros are
+    // not stored, acor_lazy), which the cvNls start that always follows it would otherwise do in a separate pass
+    // (k_vsum_zero)
     bool y_pred = false;
     void predict() {
         tn += h;
         if (tstopset && (tn - tstop) * h > 0.0) tn = tstop;
         ode::predict(n, zn, q, y, acor, s);
         y_pred = true;
+        acor_lazy = ode::lazy_ycor() != 0;
     }
     void restore(double saved_t) {
         tn = saved_t;
         ode::restore(n, zn, q, s);
-        y_pred = false;
+        y_pred = false;               // (acor_lazy kept: a failed attempt's acor is still logically +0.0)
     }
     void rescale() {
         Coefs c{};
@@ -260,6 +265,11 @@ struct shud_ode {
         rescale();
     }
 
+    bool take_lazy() {
+        const bool z = acor_lazy;
+        acor_lazy = false;
+        return z;
+    }
     // ---- cvLsSolve + SPGMR (zero guess, s1 = s2 = ewt, no preconditioner, 0 restarts) ----
     // returns 0 ok (ycor updated, del/ycor norms in h_ds), 1 recoverable failure, < 0 unrecoverable
     int ls_solve_and_update() {
@@ -267,14 +277,14 @@ struct shud_ode {
         const double bnorm = wrms_of(S_RES);
         Coefs none{};
         if (bnorm <= deltar) {                                       // cvLsSolve: small rhs
-            newton_update(n, nullptr, n, 0, none, curiter > 0 ? nullptr : delta, ewt, acor, rs(S_DEL), s);
+            newton_update(n, nullptr, n, 0, none, curiter > 0 ? nullptr : delta, ewt, acor, take_lazy(), rs(S_DEL), s);
             finalize(rs(S_DEL), 2, 0u, s);
             return fetch() ? 0 : -1;
         }
         const double delta_tol = deltar * nrmfac;
         const double r_norm = std::sqrt(h_ds[S_RES]), beta = r_norm;
         if (r_norm <= delta_tol) {                                   // SPGMR: x = x0 = 0
-            newton_update(n, nullptr, n, 0, none, nullptr, ewt, acor, rs(S_DEL), s);
+            newton_update(n, nullptr, n, 0, none, nullptr, ewt, acor, take_lazy(), rs(S_DEL), s);
             finalize(rs(S_DEL), 2, 0u, s);
             return fetch() ? 0 : -1;
         }
@@ -378,7 +388,7 @@ struct shud_ode {
         if (rv == LS_RES_REDUCED && curiter != 0) return 1;
         Coefs c{};
         for (int k = 0; k < krydim; ++k) c.c[k] = yg[k];
-        newton_update(n, V, n, krydim, c, nullptr, ewt, acor, rs(S_DEL), s);
+        newton_update(n, V, n, krydim, c, nullptr, ewt, acor, take_lazy(), rs(S_DEL), s);
         finalize(rs(S_DEL), 2, 0u, s);
         return fetch() ? 0 : -1;
     }
@@ -389,7 +399,7 @@ struct shud_ode {
         // the residual reads no ycor (identical operands, one fewer pass over HBM)
         const bool az = acor_zero;
         acor_zero = false;
-        if (az && !y_pred) vsum_zero(n, Z(0), acor, y, s);
+        if (az && !y_pred) { vsum_zero(n, Z(0), acor, y, s); acor_lazy = false; }
         else if (!az) vsum(n, Z(0), acor, y, s);
         y_pred = false;
         if (rhs(tn, y, ftemp) != 0) return SHUD_ODE_RHSFUNC_FAIL;

@@ -91,7 +91,10 @@ void normalize(int64_t n, double *w, double c, const double *ewt, const Red &r, 
 // Newton update: delta = (sum_k yg[k] V_k)/ewt (krydim > 0), or delta = dsrc (krydim 0; NULL = 0);
 // ycor += delta; r: [sum (delta*ewt)^2, sum (ycor*ewt)^2]
 void newton_update(int64_t n, const double *V, int64_t vstride, int krydim, const Coefs &yg, const double *dsrc,
-                   const double *ewt, double *ycor, const Red &r, hipStream_t s);
+                   const double *ewt, double *ycor, bool ycor_zero, const Red &r, hipStream_t s);
+// 1 when predict() leaves ycor unwritten (SHUD_ODE_LAZY_YCOR): the caller then passes ycor_zero until the first
+// newton_update after a predict
+int lazy_ycor();
 // zn[j] = l[j]*acor + zn[j], j = 0..q; if copy_to >= 0: zn[copy_to] = acor
 void complete_step(int64_t n, double *zn, const double *acor, const Coefs &l, int q, int copy_to, hipStream_t s);
 // complete_step, then ewt_set's arithmetic on the new zn[0] into ewt_next; r: [min(rtol|y| + atol), sum (y*w)^2]

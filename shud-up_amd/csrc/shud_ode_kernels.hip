@@ -33,6 +33,9 @@ static int ew_blocks(int64_t n) {
 #ifndef SHUD_ODE_NT
 #define SHUD_ODE_NT 3
 #endif
+#ifndef SHUD_ODE_LAZY_YCOR
+#define SHUD_ODE_LAZY_YCOR 1
+#endif
 template <class T>
 __device__ __forceinline__ T ldn(const T *p) {
     if (SHUD_ODE_NT & 1) return __builtin_nontemporal_load(p);
@@ -179,7 +182,10 @@ void ewt_set(int64_t n, const double *zn0, double *ewt, double rtol, double atol
 // cvPredict / cvRestore: Pascal-triangle update of the Nordsieck array in registers.  2*8*(q+1) B/entry.
 // cvPredict with y != null also performs the next cvNls start (every predict is followed by one): ycor = 0
 // (N_VConst) and y = zn[0] + ycor (N_VLinearSum) on the new zn[0] — the same add as k_vsum_zero, so -0.0
-// becomes +0.0 exactly as there — saving that pass's re-read of zn[0] (+16 B/entry here, -24 B/entry there)
+// becomes +0.0 exactly as there — saving that pass's re-read of zn[0] (+8 B/entry here, -24 B/entry there).
+// SHUD_ODE_LAZY_YCOR (default): the ycor = 0 fill is not stored at all — the controller marks ycor "all +0.0"
+// and its only readers before the first Newton update (k_residual, k_newton_update) take the zeros as operands
+// instead of loading them (identical values; -8 B/entry here and in that k_newton_update)
 template <int Q, bool FWD, int U>
 __global__ void __launch_bounds__(kThreads) k_pascal(int64_t n, double *__restrict__ zn, double *__restrict__ y,
                                                      double *__restrict__ ycor) {
@@ -198,7 +204,7 @@ __global__ void __launch_bounds__(kThreads) k_pascal(int64_t n, double *__restri
         for (int j = 0; j < Q; ++j) stn(zn + (int64_t)j * n + i, a.v[j]);
         if (FWD && y) {
             const double zero = 0.0;
-            stn(ycor + i, zero);
+            if (SHUD_ODE_LAZY_YCOR == 0) stn(ycor + i, zero);
             stn(y + i, a.v[0] + zero);
         }
     });
@@ -217,6 +223,7 @@ static void pascal(int64_t n, double *zn, int q, double *y, double *ycor, hipStr
     default: pascal_q<5, FWD>(n, zn, y, ycor, s); break;
     }
 }
+int lazy_ycor() { return SHUD_ODE_LAZY_YCOR; }
 void predict(int64_t n, double *zn, int q, double *y, double *ycor, hipStream_t s) {
     pascal<true>(n, zn, q, y, ycor, s);
 }
@@ -439,14 +446,14 @@ template <int U>
 __global__ void __launch_bounds__(kRedThreads) k_newton_update(int64_t n, const double *__restrict__ V, int64_t vstride,
                                                             int krydim, Coefs yg, const double *__restrict__ dsrc,
                                                             const double *__restrict__ ewt,
-                                                            double *__restrict__ ycor, Red r) {
+                                                            double *__restrict__ ycor, int ycor_zero, Red r) {
     double v[2] = {0.0, 0.0};
     using T = DN<kNuK + 2>;               // [0] ewt, [1] ycor, [2] dsrc (krydim 0) or [2 + k] V[k]
     const bool small = krydim <= kNuK;
     one<T>(n, [&](int64_t i) {
         T a;
         a.v[0] = ldn(ewt + i);
-        a.v[1] = ldn(ycor + i);
+        a.v[1] = ycor_zero ? 0.0 : ldn(ycor + i);          // ycor_zero: ycor is all +0.0 (lazy cvNls start)
         if (krydim == 0) {
             a.v[2] = dsrc ? ldn(dsrc + i) : 0.0;
         } else if (small) {
@@ -480,8 +487,8 @@ __global__ void __launch_bounds__(kRedThreads) k_newton_update(int64_t n, const 
     block_partial<2>(v, 0u, r);
 }
 void newton_update(int64_t n, const double *V, int64_t vstride, int krydim, const Coefs &yg, const double *dsrc,
-                   const double *ewt, double *ycor, const Red &r, hipStream_t s) {
-    LAUNCH_RED(k_newton_update, r, s, n, V, vstride, krydim, yg, dsrc, ewt, ycor);
+                   const double *ewt, double *ycor, bool ycor_zero, const Red &r, hipStream_t s) {
+    LAUNCH_RED(k_newton_update, r, s, n, V, vstride, krydim, yg, dsrc, ewt, ycor, (int)ycor_zero);
 }
 
 // cvCompleteStep: zn[j] = l[j]*acor + zn[j] (N_VScaleAddMulti), optional zn[qmax] = acor.
