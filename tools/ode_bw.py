@@ -6,6 +6,7 @@ k_complete) are priced at --q (the order the run mostly used).  usage:
 import argparse
 import csv
 import re
+import sys
 
 # bytes per entry; callables take the order q
 PER_ENTRY = {
@@ -32,6 +33,7 @@ def main():
     ap.add_argument("csv")
     ap.add_argument("ny", type=int)
     ap.add_argument("--q", type=int, default=3)
+    ap.add_argument("--eager-ycor", action="store_true", help="sources before the lazy ycor (predict stores ycor = 0)")
     ap.add_argument("--copy-gbs", type=float, default=6400.0, help="the box's STREAM copy rate")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.csv)))
@@ -44,7 +46,8 @@ def main():
             mm = re.search(r"k_pascal<(\d), (true|false)", name)
             q = int(mm.group(1))
             fwd = mm.group(2) == "true"
-            b = 8 * (2 * q + 1) + (16 if fwd else 0)      # predict also writes y and ycor (round 3)
+            lazy = "--eager-ycor" not in sys.argv
+            b = 8 * (2 * q + 1) + ((8 if lazy else 16) if fwd else 0)   # predict also writes y (+ ycor unless lazy)
             key = f"k_pascal<{q},{'pred' if fwd else 'rest'}>"
         elif m and m.group(1) in PER_ENTRY:
             key = m.group(1)
