@@ -4,9 +4,14 @@
 Workload (BASELINE.json north_star / SURVEY §8d): synthetic 10M-triangle mesh (syn-10M: 3162 x 1582 quads,
 ccw-like river density, seed 12345), seeded random state y and ET-step inputs, serial (reference `make
 shud`) semantics.  One "step" = one RHS evaluation f(t, y, ydot) with y / ydot resident in HBM.
-N = 1: the whole mesh on one GPU.  N > 1 (torch.distributed.run, one process per GPU): the same 10M mesh
+N = 1: the whole mesh on one GPU.  N > 1 (one process per GPU: under torch.distributed.run, or — `--gpus N`
+without a launcher — started by bench.py itself before any GPU call, see launch_ranks): the same 10M mesh
 partitioned by the C++ partitioner (multilevel or RCB, whichever gives the smaller largest halo) across the N ranks, ghost states exchanged by RCCL (grouped send/recv over xGMI) inside
 every RHS call; value = NumEle_total x K / max-over-ranks time ("scaling": "strong": the 10M mesh is fixed).
+
+At N > 1 (and with --partition-1) every rank's DY is then checked bit for bit against a full-mesh single-GPU
+handle on its own device (`parity_vs_1gpu`); a fatal error flag on any rank (incl. a timed-out halo poll) or a
+parity miss ends the run with a non-zero status and no result line.
 
 Prints ONE JSON line on rank 0 with roofline (dominant kernel: shud_ele_kernel, HIP-event timed on the
 stream it runs on) and cpu_baseline (the CPU restatement oracle on this host's cores, bounded sample).
@@ -52,12 +57,58 @@ def shared_partition(gm, world, rank, dist=None, device="cpu"):
     return ele_part, pst
 
 
-def main():
-    # stdout carries exactly one JSON line: libraries that print banners on it (RCCL prints its version block
-    # at communicator init) write to stderr instead until the line is printed
+FATAL_FLAGS = 0x01 | 0x02 | 0x04 | 0x08 | 0x80   # SHUD_EF_NAN_QELE | EFFKH | ET_NEG | ET_NAN | HALO_WAIT (shud_rhs.h)
+
+
+def launch_ranks(nproc, argv, dry):
+    """`--gpus N > 1` without a launcher: start the N rank processes here (one per GPU, RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* in their environment, rendezvous on 127.0.0.1) BEFORE anything touches the GPU, forward
+    the ranks' stdout (rank 0's JSON line) and exit with the first non-zero rank status (the others are then
+    terminated).  This process never initialises HIP."""
+    import socket
+    import subprocess
+    import threading
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs, outs = [], []
+    for r in range(nproc):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc), LOCAL_WORLD_SIZE=str(nproc),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SHUD_BENCH_LAUNCHED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=subprocess.PIPE, text=True))
+        outs.append([])
+
+    def pump(k):
+        for line in procs[k].stdout:
+            outs[k].append(line)
+    th = [threading.Thread(target=pump, args=(k,), daemon=True) for k in range(nproc)]
+    for t in th:
+        t.start()
+    rc = 0
+    live = set(range(nproc))
+    while live:
+        for k in sorted(live):
+            st = procs[k].poll()
+            if st is None:
+                continue
+            live.discard(k)
+            if st != 0 and rc == 0:
+                rc = st if st > 0 else 128 - st
+                print(f"[bench] rank {k} exited with status {st}: stopping the other ranks", file=sys.stderr,
+                      flush=True)
+                for j in live:
+                    procs[j].terminate()
+        time.sleep(0.05)
+    for t in th:
+        t.join(timeout=5)
+    for k in range(nproc) if dry else [0]:
+        sys.stdout.write("".join(outs[k]))
     sys.stdout.flush()
-    json_fd = os.dup(1)
-    os.dup2(2, 1)
+    return rc
+
+
+def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
@@ -79,13 +130,32 @@ def main():
                     help="elements of the end-to-end shud_gpu run (C++ host, one simulated day); 0 = skip")
     ap.add_argument("--partition-1", action="store_true",
                     help="run the N>1 code path (partitioned handle, RCCL comm, overlap) with one rank (smoke test)")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="N>1 / --partition-1: skip the bit-identity check of every rank's DY against a full-mesh "
+                         "single-GPU handle")
+    ap.add_argument("--dry-launch", action="store_true",
+                    help="launcher test: each rank reports RANK / WORLD_SIZE and exits before touching the GPU")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.dry_launch))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+        print(f"[bench] error: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if args.dry_launch:
+        print(json.dumps({"dry_launch": True, "rank": rank, "world_size": world, "local_rank": local,
+                          "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}"}), flush=True)
+        if os.environ.get("SHUD_BENCH_DRY_FAIL_RANK") == str(rank):    # launcher test: a failing rank
+            sys.exit(5)
+        return
+    # stdout carries exactly one JSON line: libraries that print banners on it (RCCL prints its version block
+    # at communicator init) write to stderr instead until the line is printed
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
 
     import torch
     import torch.distributed as dist
@@ -174,9 +244,23 @@ def main():
         kt = torch.tensor([ms_ele_loop, ms_riv_loop, ms_eval_loop], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(kt, op=dist.ReduceOp.MAX)
         kmax = {"shud_ele_kernel": float(kt[0]), "shud_riv_kernel": float(kt[1]), "eval": float(kt[2])}
+    # a fatal error flag (NaN fluxes, effKH range, ET checks, a timed-out halo poll) means the timed evals computed
+    # wrong DY: no throughput line, non-zero exit on every rank
     err = h.get_error()
-    if err["exit_code"]:
-        log(f"[bench] WARNING physics error flags {err}")
+    fatal = int(err["flags"]) & FATAL_FLAGS
+    if world > 1:
+        tf = torch.tensor([fatal], dtype=torch.int64, device=f"cuda:{local}")
+        dist.all_reduce(tf, op=dist.ReduceOp.MAX)
+        fatal = int(tf.item())
+    if fatal:
+        print(f"[bench] rank {rank}: fatal error flags 0x{fatal:x} (this rank: {err}) — no result", file=sys.stderr,
+              flush=True)
+        sys.exit(3)
+    parity = None
+    if (world > 1 or args.partition_1) and not args.no_parity:
+        parity = parity_vs_1gpu(h, gm, y_glob, part, mode, local, stream, yp, dyp, dy_t, dist if world > 1 else None)
+        if not parity["ok"]:
+            print(f"[bench] rank {rank}: DY differs from the single-GPU handle: {parity}", file=sys.stderr, flush=True)
 
     # per-kernel times: HIP events recorded inside the timed loop on the handle's stream (= torch's current
     # stream); a partitioned handle also gets a serialized per-phase breakdown (halo exchange alone)
@@ -241,6 +325,15 @@ def main():
         },
         "cpu_baseline": None,
     }
+    if world > 1 or args.partition_1:
+        out["rccl_ranks"] = world
+        out["parity_vs_1gpu"] = None if parity is None else parity["all_ok"]
+        if parity is not None:
+            out["parity_detail"] = {k: parity[k] for k in ("calls", "words_checked_rank0", "ranks_ok", "note")}
+        if parity is not None and not parity["all_ok"]:
+            sys.stdout.flush()
+            print(json.dumps(out), file=sys.stderr, flush=True)
+            sys.exit(4)
     # the practical HBM ceilings on this box (measured before the warm-up, see there)
     if sp:
         out["roofline"].update(sp)
@@ -299,6 +392,45 @@ def main():
         h.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def parity_vs_1gpu(h, gm, y_glob, part, mode, local, stream, yp, dyp, dy_t, dist, calls=2):
+    """After the timed loop: every rank's owned DY, bit for bit, against a full-mesh single-GPU handle evaluated on
+    the rank's own device at the same global state.  Both handles restart from the same step inputs and carried
+    state (set_step_inputs), then make `calls` successive stateful evaluations; the partitioned ones run the full
+    device eval (pack, RCCL exchange, folded launch) collectively across the ranks."""
+    import torch
+    from shud_rhs import partition, runtime
+    h.set_step_inputs()
+    full = runtime.RhsHandle(gm, mode=mode, device=local, stream=stream.cuda_stream)
+    full.set_step_inputs()
+    yg = torch.from_numpy(y_glob).to(f"cuda:{local}")
+    dyg = torch.empty_like(yg)
+    ok, words = True, 0
+    for _ in range(calls):
+        h.eval_device(0.0, yp, dyp)
+        full.eval_device(0.0, yg.data_ptr(), dyg.data_ptr())
+        torch.cuda.synchronize()
+        got = dy_t.cpu().numpy()
+        want = partition.local_state(dyg.cpu().numpy(), gm, part)
+        ok &= bool(np.array_equal(got, want, equal_nan=True))
+        words += got.size
+    e1, e2 = h.get_error(), full.get_error()
+    ok &= not (int(e1["flags"]) & FATAL_FLAGS) and int(e1["flags"]) == int(e2["flags"])
+    full.close()
+    del yg, dyg
+    torch.cuda.empty_cache()
+    n_ok = 1 if ok else 0
+    if dist is not None:
+        t = torch.tensor([n_ok], dtype=torch.int64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        n_ok = int(t.item())
+        world = dist.get_world_size()
+    else:
+        world = 1
+    return {"ok": ok, "all_ok": n_ok == world, "ranks_ok": n_ok, "calls": calls, "words_checked_rank0": words,
+            "note": "each rank's owned DY after set_step_inputs + 2 stateful device evals (RCCL exchange, folded "
+                    "launch) vs a full-mesh single-GPU handle on the same device: np.array_equal (NaN == NaN)"}
 
 
 def e2e_timing(n_ele, days=1.0):

@@ -243,6 +243,14 @@ int  shud_rhs_halo_buffers(shud_rhs_t h, double **ele_send, double **riv_send, d
                            double **riv_ghost);
 int  shud_rhs_eval_pack(shud_rhs_t h, const double *d_y);
 int  shud_rhs_eval_compute(shud_rhs_t h, double t, const double *d_y, double *d_ydot);
+/* Test hook (no reference analogue; tests/test_gpu_partition.py): on every following device eval of a
+ * partitioned handle the comm stream, after its pack (and RCCL exchange), spins spin_us microseconds, then copies
+ * the ghost states from d_ele_src (3 x #ghost elements, recv order) / d_riv_src (#ghost reaches) into the ghost
+ * buffers with a kernel (NULL: no copy), then publishes the halo flag unless publish == 0 (the folded launch's
+ * boundary workgroups then time out: SHUD_EF_HALO_WAIT).  timeout_ms > 0 sets their poll bound (else
+ * SHUD_HALO_TIMEOUT_MS or 5000).  spin_us 0, NULL sources and publish 1 disarm the hook. */
+int  shud_rhs_debug_halo(shud_rhs_t h, double spin_us, const double *d_ele_src, const double *d_riv_src,
+                         int publish, double timeout_ms);
 
 int  shud_rhs_nccl_unique_id(char out[128]);
 int  shud_rhs_create_partitioned(const ShudMeshSoA *mesh, const ShudParamsSoA *par,

@@ -175,11 +175,16 @@ void launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YV
 struct HaloWait {
     const unsigned long long *flag;
     unsigned long long epoch;
+    unsigned long long timeout;          // wall_clock64() ticks a boundary wave polls before SHUD_EF_HALO_WAIT
 };
 bool launch_element_kernel_packed_fold(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int n_int,
                                        int n_all, int cur, int mode, bool open, bool fu_unit, const DevDiag &dg,
                                        const HaloWait &hw, hipStream_t s);
 void launch_halo_flag(unsigned long long *flag, unsigned long long epoch, hipStream_t s);
+// test hooks (shud_rhs_debug_halo): a one-lane spin of `ticks` wall-clock ticks, and a plain vector copy (the
+// stand-in for RCCL's receive kernels writing the ghost buffers), both on the comm stream
+void launch_spin(unsigned long long ticks, hipStream_t s);
+void launch_copy_f64(double *dst, const double *src, size_t n, hipStream_t s);
 void launch_river_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int mode,
                                 bool diag, const DevDiag &dg, hipStream_t s);
 void launch_lake_kernel(const DevMesh &m, const DevPacked &p, const DevLake &L, const YView &Y, double *dy,

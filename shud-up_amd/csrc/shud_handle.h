@@ -92,7 +92,15 @@ struct shud_rhs {
     // boundary + ghost elements folded into the interior launch (launch_element_kernel_packed_fold): the comm stream
     // publishes halo_epoch into d_halo_flag after the exchange; SHUD_RHS_FOLD=0 keeps two launches (A/B)
     bool fold = false;
+    bool fold_join = false;              // main stream joins ev_comm after the folded eval (SHUD_RHS_FOLD_JOIN=1)
     unsigned long long *d_halo_flag = nullptr, halo_epoch = 0;
+    unsigned long long halo_timeout = 0; // poll bound in wall_clock64 ticks (SHUD_HALO_TIMEOUT_MS, default 5000)
+    double wall_khz = 100000.0;          // hipDeviceAttributeWallClockRate
+    long long n_exch = 0;                // exchanges enqueued (an RCCL handle's first one takes the split path)
+    // test hook (shud_rhs_debug_halo): a late or missing halo on the comm stream
+    bool dbg_armed = false, dbg_publish = true;
+    unsigned long long dbg_spin = 0;
+    const double *dbg_gele = nullptr, *dbg_griv = nullptr;
     // in-loop kernel timing (shud_rhs_timing): 3 events per device eval {start, after element kernel(s),
     // after river (+lake) kernel}, recorded on the handle's stream while enabled
     int tm_cap = 0, tm_n = 0, tm_stride = 1;

@@ -622,7 +622,7 @@ void dky(int64_t n, const double *zn, int64_t stride, const int *jsv, const Coef
          double *out, hipStream_t s) {
     Js js{};
     for (int k = 0; k < nvec && k <= kQMax; ++k) js.j[k] = jsv[k];
-    k_dky<<<grid_blocks(n), kThreads, 0, s>>>(n, zn, stride, js, c, nvec, rscale, out);
+    k_dky<<<ew_blocks(n), kThreads, 0, s>>>(n, zn, stride, js, c, nvec, rscale, out);   // one entry per thread
 }
 
 }  // namespace ode

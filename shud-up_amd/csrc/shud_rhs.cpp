@@ -674,6 +674,18 @@ static int setup_partition(shud_rhs *h, const ShudPartition *part) {
     if ((rc = h->upload(&h->d_halo_flag, (const unsigned long long *)nullptr, 1))) return rc;
     const char *fe = getenv("SHUD_RHS_FOLD");
     h->fold = !(fe && fe[0] == '0');
+    // the trailing join of the comm stream after a folded eval costs ~4 us per eval at 8 ranks (one more packet for
+    // the command processor between evals; profiles/r04/rankjoin): off by default.  Without it, after a poll timeout
+    // (SHUD_EF_HALO_WAIT, fatal) the late pack / exchange may still run beside later main-stream work — results that
+    // the fatal flag already invalidates; the error read (shud_read_err) drains the comm stream before reporting
+    const char *fj = getenv("SHUD_RHS_FOLD_JOIN");
+    h->fold_join = fj && fj[0] == '1';
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device) == hipSuccess && khz > 0)
+        h->wall_khz = khz;
+    const char *tm = getenv("SHUD_HALO_TIMEOUT_MS");
+    const double ms = (tm && atof(tm) > 0) ? atof(tm) : 5000.0;
+    h->halo_timeout = (unsigned long long)(ms * h->wall_khz);
     return 0;
 }
 
@@ -804,8 +816,15 @@ static int exchange(shud_rhs *h, const double *y) {
     }
     NCCL_TRY(ncclGroupEnd());
     }                                // external transport (tests): the caller placed the ghost buffers
-    if (h->fold) launch_halo_flag(h->d_halo_flag, ++h->halo_epoch, h->s_comm);
+    if (h->dbg_armed) {              // test hook: the halo arrives late (spin), written by a kernel, or never
+        if (h->dbg_spin) launch_spin(h->dbg_spin, h->s_comm);
+        if (h->dbg_gele) launch_copy_f64(h->d_gele, h->dbg_gele, 3 * (size_t)h->n_eghost, h->s_comm);
+        if (h->dbg_griv) launch_copy_f64(h->d_griv, h->dbg_griv, (size_t)h->n_rghost, h->s_comm);
+    }
+    ++h->halo_epoch;
+    if (h->fold && !(h->dbg_armed && !h->dbg_publish)) launch_halo_flag(h->d_halo_flag, h->halo_epoch, h->s_comm);
     HIP_TRY(hipEventRecord(h->ev_comm, h->s_comm));
+    h->n_exch++;
     return 0;
 }
 
@@ -850,6 +869,9 @@ int shud_read_err(shud_rhs *h) {
         HIP_TRY(hipStreamSynchronize(h->stream));
         for (int k = 0; k < kWarnSlots; k++) h->h_err->n_warn += h->h_warn[k * kWarnStride];
     }
+    // a halo poll timed out: the pack / exchange it gave up on may still be running — drain the comm stream before
+    // the failure reaches the caller, so nothing of that eval is still in flight when the caller reacts
+    if ((h->h_err->flags & SHUD_EF_HALO_WAIT) && h->s_comm) HIP_TRY(hipStreamSynchronize(h->s_comm));
     return 0;
 }
 static int read_err(shud_rhs *h) { return shud_read_err(h); }
@@ -866,14 +888,20 @@ static const uint32_t kFatal = SHUD_EF_NAN_QELE | SHUD_EF_EFFKH | SHUD_EF_ET_NEG
 // launch's boundary workgroups then skip the flag
 static int launch_split(shud_rhs *h, const double *y, double *dy, hipEvent_t e_mid = nullptr,
                         bool stream_halo = false) {
-    if (h->fold && h->packed && !h->variant && !h->lakeon && !SHUD_ABL_NOSPLIT) {
+    // an RCCL communicator connects its peers lazily on the first send/recv (can take far longer than any eval):
+    // that first exchange is waited for on the stream (split path), never polled by workgroups
+    const bool first_rccl = h->use_nccl && h->n_exch <= 1 && !stream_halo;
+    if (h->fold && h->packed && !h->variant && !h->lakeon && !SHUD_ABL_NOSPLIT && !first_rccl) {
         YView Y{y, h->d_gele, h->d_griv, h->n_own, h->n_own_riv};
-        const HaloWait hw{h->d_halo_flag, stream_halo ? 0ull : h->halo_epoch};
+        const HaloWait hw{h->d_halo_flag, stream_halo ? 0ull : h->halo_epoch, h->halo_timeout};
         if (launch_element_kernel_packed_fold(h->dm, h->dp, Y, dy, h->n_int, h->n_own + h->n_segghost, h->cur,
                                               h->mode, h->open, h->fu_unit[0] && h->fu_unit[1], h->dd, hw,
                                               h->stream)) {
             if (e_mid) HIP_TRY(hipEventRecord(e_mid, h->stream));
             launch_riv(h, y, dy, false);             // after the boundary workgroups, which saw the halo
+            // optional join of the comm stream (normally complete long before: the boundary workgroups saw its flag),
+            // so that after a poll timeout no later main-stream work runs beside the late pack / exchange
+            if (h->fold_join && !stream_halo) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_comm, 0));
             HIP_TRY(hipGetLastError());
             return 0;
         }
@@ -1126,6 +1154,24 @@ extern "C" void *shud_rhs_stream(shud_rhs_t h) { return h ? (void *)h->stream : 
 extern "C" int shud_rhs_halo_buffers(shud_rhs_t h, double **esend, double **rsend, double **gele, double **griv) {
     if (!h || !h->partitioned) return shud_fail(SHUD_ERR_ARG, "not a partitioned handle");
     *esend = h->d_esend; *rsend = h->d_rsend; *gele = h->d_gele; *griv = h->d_griv;
+    return SHUD_OK;
+}
+// test hook: a late, kernel-written or missing halo on the comm stream of every following device eval
+extern "C" int shud_rhs_debug_halo(shud_rhs_t h, double spin_us, const double *d_ele_src, const double *d_riv_src,
+                                   int publish, double timeout_ms) {
+    if (!h || !h->partitioned) return shud_fail(SHUD_ERR_ARG, "not a partitioned handle");
+    if (spin_us < 0 || spin_us > 1e7) return shud_fail(SHUD_ERR_ARG, "spin_us out of range");
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hipStreamSynchronize(h->s_comm));
+    h->dbg_spin = (unsigned long long)(spin_us * 1e-3 * h->wall_khz);
+    h->dbg_gele = d_ele_src;
+    h->dbg_griv = d_riv_src;
+    h->dbg_publish = publish != 0;
+    h->dbg_armed = h->dbg_spin || d_ele_src || d_riv_src || !h->dbg_publish;
+    const char *tm = getenv("SHUD_HALO_TIMEOUT_MS");
+    const double ms = timeout_ms > 0 ? timeout_ms : (tm && atof(tm) > 0) ? atof(tm) : 5000.0;
+    h->halo_timeout = (unsigned long long)(ms * h->wall_khz);
     return SHUD_OK;
 }
 // split eval for external transport: pack, (caller exchanges), compute

@@ -107,11 +107,16 @@ std::vector<double> test_state(const double *y0, int64_t ny, int ne, int k) {
     return y;
 }
 
-// the RCCL id file of one job: "<token>\n" + 128 id bytes.  The token names the job (torchrun's run id and the
-// rendezvous address), so a file left by an earlier job in the same outdir is never taken for this one's
+// the RCCL id file of one job: "<token>\n" + 128 id bytes.  The token names the job: torchrun's run id, the
+// rendezvous address and the launcher's pid (every local rank of one job is a child of the same launcher process —
+// torchrun's agent or bench.py — and a later job's launcher is another process; static rendezvous leaves the run id
+// at "none", so address and port alone would accept an earlier job's file).  SHUD_JOB_ID, when set by the caller,
+// replaces the launcher pid.
 std::string job_token() {
     const char *run = getenv("TORCHELASTIC_RUN_ID"), *ma = getenv("MASTER_ADDR"), *mp = getenv("MASTER_PORT");
-    return std::string(run ? run : "-") + ":" + (ma ? ma : "-") + ":" + (mp ? mp : "-");
+    const char *jid = getenv("SHUD_JOB_ID");
+    const std::string who = jid ? std::string(jid) : "ppid" + std::to_string((long)getppid());
+    return std::string(run ? run : "-") + ":" + (ma ? ma : "-") + ":" + (mp ? mp : "-") + ":" + who;
 }
 
 // the 128 id bytes of `f` if it carries `token` and was written after `not_before` (seconds since the epoch)

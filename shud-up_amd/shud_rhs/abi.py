@@ -188,6 +188,7 @@ FUNCTIONS = {
                                         C.POINTER(C.c_void_p)]),
     "shud_rhs_eval_pack": (C.c_int, [_H, C.c_void_p]),
     "shud_rhs_eval_compute": (C.c_int, [_H, C.c_double, C.c_void_p, C.c_void_p]),
+    "shud_rhs_debug_halo": (C.c_int, [_H, C.c_double, C.c_void_p, C.c_void_p, C.c_int, C.c_double]),
 }
 # include/shud_et.h
 ET_FUNCTIONS = {

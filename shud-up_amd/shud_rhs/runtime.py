@@ -233,6 +233,11 @@ class RhsHandle:
     def eval_compute(self, t, d_y, d_ydot):
         _check(lib().shud_rhs_eval_compute(self.h, float(t), C.c_void_p(d_y), C.c_void_p(d_ydot)), "eval_compute")
 
+    def debug_halo(self, spin_us=0.0, d_ele_src=None, d_riv_src=None, publish=True, timeout_ms=0.0):
+        """test hook (shud_rhs_debug_halo): late / kernel-written / missing halo on the comm stream"""
+        _check(lib().shud_rhs_debug_halo(self.h, float(spin_us), C.c_void_p(d_ele_src), C.c_void_p(d_riv_src),
+                                         1 if publish else 0, float(timeout_ms)), "debug_halo")
+
 
 def nccl_unique_id():
     buf = C.create_string_buffer(128)

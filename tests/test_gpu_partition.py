@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 import cases
-from shud_rhs import partition, workload
+from shud_rhs import abi, partition, workload
 
 pytestmark = pytest.mark.gpu
 
@@ -208,3 +208,98 @@ def test_rccl_comm_single_rank(mode):
         h.device_free(dy_)
         h.device_free(ddy)
         h.close()
+
+
+def _late_halo_ranks(m, nranks):
+    ep, _ = partition.cpp_partition(m, nranks, partition.PART_AUTO)
+    return [partition.CppPlan(m, ep, nranks, r).local_model() for r in range(nranks)]
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_folded_halo_late(mode, monkeypatch):
+    """The folded launch's halo hand-off with a genuinely LATE halo (VERDICT r03 item 2, MI355X guide: test every
+    hand-off under uneven load, checking every word): each rank's comm stream spins ~200 us after its pack, then a
+    kernel writes the ghost states (as RCCL's receive kernels would) and only then publishes the flag, so the boundary
+    workgroups really poll while the interior workgroups run.  The ghost values change on every eval (a new state
+    per call), so a stale line shows up; every owned DY word must equal the single handle's."""
+    from shud_rhs import runtime as rt
+    monkeypatch.setenv("SHUD_RHS_FOLD", "1")
+    m, y = cases.variant(20000, seed=29)
+    locs = _late_halo_ranks(m, 4)
+    single = rt.RhsHandle(m, mode=mode)
+    single.set_step_inputs()
+    hs, bufs = [], []
+    try:
+        for lm, part in locs:
+            h = rt.RhsHandle(lm, mode=mode, partition=part)
+            h.set_step_inputs()
+            ny = 3 * part.n_own_ele + part.n_own_riv
+            ge, gr = partition.ghost_values(y, m, part)
+            st_e, st_r = h.device_alloc(8 * max(1, ge.size)), h.device_alloc(8 * max(1, gr.size))
+            bufs.append((h.device_alloc(8 * ny), h.device_alloc(8 * ny), ny, st_e, st_r))
+            h.debug_halo(spin_us=200.0, d_ele_src=st_e, d_riv_src=st_r)
+            hs.append(h)
+        states = [workload.random_state(m, seed=100 + k) for k in range(6)]
+        for call, yy in enumerate(states):            # a different state (and halo) on every stateful call
+            ref = single.eval(0.0, yy)
+            for r, (lm, part) in enumerate(locs):
+                yb, dyb, ny, st_e, st_r = bufs[r]
+                ge, gr = partition.ghost_values(yy, m, part)
+                hs[r].h2d(yb, partition.local_state(yy, m, part))
+                if ge.size:
+                    hs[r].h2d(st_e, ge)
+                if gr.size:
+                    hs[r].h2d(st_r, gr)
+                hs[r].eval_device(0.0, yb, dyb)
+            for r, (lm, part) in enumerate(locs):
+                yb, dyb, ny, _, _ = bufs[r]
+                got = hs[r].d2h(np.zeros(ny), dyb)
+                e = hs[r].get_error()
+                assert e["flags"] & 0x80 == 0, f"rank {r} call {call}: SHUD_EF_HALO_WAIT"
+                want = partition.local_state(ref, m, part)
+                assert np.array_equal(got, want, equal_nan=True), \
+                    f"rank {r} call {call}: {(~((got == want) | (np.isnan(got) & np.isnan(want)))).sum()} words differ"
+    finally:
+        for h, b in zip(hs, bufs):
+            for p in (b[0], b[1], b[3], b[4]):
+                h.device_free(p)
+            h.close()
+        single.close()
+
+
+def test_folded_halo_never_arrives(monkeypatch):
+    """The flag never comes: the boundary workgroups' bounded poll ends in the fatal SHUD_EF_HALO_WAIT and the eval
+    returns an error (SHUD_ERR_PHYSICS); with the hook disarmed the next evals are bit-identical again."""
+    from shud_rhs import runtime as rt
+    monkeypatch.setenv("SHUD_RHS_FOLD", "1")
+    m, y = cases.variant(20000, seed=31)
+    lm, part = _late_halo_ranks(m, 2)[1]
+    single = rt.RhsHandle(m)
+    single.set_step_inputs()
+    h = rt.RhsHandle(lm, partition=part)
+    h.set_step_inputs()
+    ge, gr = partition.ghost_values(y, m, part)
+    st_e, st_r = h.device_alloc(8 * max(1, ge.size)), h.device_alloc(8 * max(1, gr.size))
+    try:
+        h.h2d(st_e, ge)
+        h.h2d(st_r, gr)
+        h.debug_halo(d_ele_src=st_e, d_riv_src=st_r, publish=False, timeout_ms=20.0)
+        with pytest.raises(rt.ShudRhsError) as ei:
+            h.eval(0.0, partition.local_state(y, m, part))
+        assert ei.value.code == abi.SHUD_ERR_PHYSICS
+        assert h.get_error()["flags"] & 0x80, "SHUD_EF_HALO_WAIT not raised"
+        h.clear_error()
+        # recovery: the flag is published again; both handles restart from the same step inputs / carried state
+        h.debug_halo(d_ele_src=st_e, d_riv_src=st_r, publish=True)
+        h.set_step_inputs()
+        single.set_step_inputs()
+        for call in range(2):
+            ref = single.eval(0.0, y)
+            got = h.eval(0.0, partition.local_state(y, m, part))
+            assert np.array_equal(got, partition.local_state(ref, m, part), equal_nan=True), f"call {call}"
+        assert h.get_error()["flags"] & 0x80 == 0
+    finally:
+        h.device_free(st_e)
+        h.device_free(st_r)
+        h.close()
+        single.close()

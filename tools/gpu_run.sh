@@ -15,6 +15,7 @@
 #   sq           SQ / GRBM counter passes (tools/sq_counters.sh)          ode   integrator kernel trace
 #   part1        bench's N>1 code path on one rank                        rank  tools/rank_timing.py (2/4/8-way)
 #   rankab:L1,L2 tools/rank_timing.py 8 for the production lib and each A/B lib   rankkt  its kernel trace (8-way)
+#   rankjoin     8-way rank timing with / without the trailing comm-stream join (SHUD_RHS_FOLD_JOIN=1: join)
 #   rankfold     8-way rank timing, boundary elements folded into the interior launch vs split (SHUD_RHS_FOLD=0)
 #   syn1m        tools/profile_1m.sh (BASELINE configs[3]: bench line, kernel trace, PMC)   sizes  RHS lines at 1.25/2.5/5M + OMP
 #   e2e          tools/profile_e2e.sh 1M, 1 day                          redbench  tools/ode_red_bench (reduction forms)
@@ -74,6 +75,9 @@ for step in "$@"; do
     rankfold)                   # 8-way rank timing with the boundary launch folded (default) and split
       timeout -k 10 300 python tools/rank_timing.py 8 > "$O/rank8_fold.json" 2> "$O/rank8_fold.err"
       SHUD_RHS_FOLD=0 timeout -k 10 300 python tools/rank_timing.py 8 > "$O/rank8_split.json" 2> "$O/rank8_split.err" ;;
+    rankjoin)                   # 8-way rank timing with / without the main stream's trailing join of the comm stream
+      SHUD_RHS_FOLD_JOIN=1 timeout -k 10 300 python tools/rank_timing.py 8 > "$O/rank8_join.json" 2> "$O/rank8_join.err"
+      timeout -k 10 300 python tools/rank_timing.py 8 > "$O/rank8_nojoin.json" 2> "$O/rank8_nojoin.err" ;;
     rankkt) timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d "$O/rankkt" -o run -- python3 tools/rank_timing.py 8 > "$O/rankkt.json" 2> "$O/rankkt.err" ;;
     pmc)
       timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch" -o run -- python3 bench.py $A --steps 5 --warmup 1 > "$O/pmc_fetch.log" 2>&1
