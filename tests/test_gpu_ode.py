@@ -231,25 +231,25 @@ def test_physics_error_surfaces():
 def test_ccw_one_day_trajectory(mode):
     """One simulated day (144 solver steps) of ccw, device chain vs CPU oracle chain (tests/traj.py).
 
-    Measured (profiles/r02/traj_ccw_day.json): the chains agree to ~1e-13 of the error weight for the first
-    steps; OCML-vs-glibc ulps in pow/cbrt then grow ~10x per solver step through the carried u_satn / qEleE_IC
-    feedback (serial) until, after ~2-3 h serial / ~17 h OMP, the two runs take different internal step
-    sequences and become two independent CVODE solutions of the same problem.  From then on the difference is
-    set by the integration tolerance, not by rounding: each run keeps its local error within 1 weighted unit
-    per step, so the weighted difference stays O(1) and the water volume (area-weighted surface + Sy x (unsat +
-    GW)) agrees to ~1e-7 (serial) / ~1e-8 (OMP).  Which O(1) value a given output time shows depends on where the
-    two step sequences happen to stand: round 2's reduction order gave a max of 3.1 serial / 1.9 OMP, round 3's
-    (one entry per thread, profiles/r03/traj/) 13.7 serial at the very last output only (95th percentile over the
-    day 2.5) and 2.1 OMP.  Bounds asserted: 95th percentile of the weighted difference over the day <= 5 and its
-    max <= 50 (a few / tens of times the solver's own per-step tolerance), volume <= 1e-5 relative, the first
-    hour within 1e-6 of the error weight, both chains finishing every step, step counts within 10 %."""
+    The chains agree to ~1e-13 of the error weight for the first steps; OCML-vs-glibc ulps in pow/cbrt then grow
+    through the carried u_satn / qEleE_IC feedback (serial) until the two runs take different internal step
+    sequences and become two independent CVODE solutions of the same problem, whose difference is set by the
+    integration tolerance, not by rounding.  The bound is MEASURED, not chosen: traj.spread
+    runs the oracle chain against itself with the other reduction order and from initial states one ulp away
+    (CPU only, ~20 s), i.e. what rounding-level differences alone do to this problem over the day
+    (profiles/r04/traj/spread.json: serial envelope max 13.1 / p95 3.7, OMP 5.9 / 5.8).  Asserted: the device
+    chain's max and 95th-percentile weighted difference over the day are within twice that envelope, the first
+    hour within 1e-6 of the error weight (tighter than any ulp-perturbed CPU chain reaches), water volume within
+    1e-5 relative, both chains finishing every step, step counts within 10 %."""
     import traj
+    env = traj.spread(mode)["envelope"]
     rows = traj.run(mode)
     assert len(rows) == 144
     assert all(r["flag_dev"] == r["flag_cpu"] == 0 for r in rows)
     assert max(r["werr"] for r in rows[:6]) <= 1e-6
     werr = np.array([r["werr"] for r in rows])
-    assert np.percentile(werr, 95) <= 5.0 and werr.max() <= 50.0, (np.percentile(werr, 95), werr.max())
+    assert werr.max() <= 2.0 * env["max"], (werr.max(), env)
+    assert np.percentile(werr, 95) <= 2.0 * env["p95"], (np.percentile(werr, 95), env)
     assert max(r["vol_rel"] for r in rows) <= 1e-5
     nd, nc = rows[-1]["nst"]
     assert abs(nd - nc) <= 0.1 * nc

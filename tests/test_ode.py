@@ -141,3 +141,15 @@ def test_device_reduction_order_restatement():
     assert np.all(np.abs(y1 - y0_) <= 1e-9 * np.abs(y0_) + 1e-15)
     ex = y0 * np.exp(-lam * 0.002)
     assert np.all(np.abs(y1 - ex) <= 2e-4 * np.abs(ex) + 1e-8)
+
+
+def test_trajectory_spread_reproduces_committed_measurement():
+    """The envelope the one-day device trajectory test is bounded by (tests/traj.py spread, CPU oracle chains under
+    rounding-level changes) is deterministic and equals the committed measurement profiles/r04/traj/spread.json."""
+    import json
+    import os
+    import traj
+    ref = json.load(open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                      "profiles", "r04", "traj", "spread.json")))
+    got = traj.spread(0)
+    assert got == ref["serial"]

@@ -38,3 +38,40 @@ def run(mode, nsteps=144, dt=10.0):
     d.close()
     h.close()
     return rows
+
+
+def _cpu_chain(mode, order, y0, nsteps, dt):
+    import cases
+    import oracle
+    oracle.OracleOde.set_reduction_order(order)
+    m, _ = cases.ccw()
+    r = oracle.OracleRhs(m, mode)
+    r.set_step_inputs()
+    o = oracle.OracleOde(r, 0.0, y0, 1e-4, 1e-4, 1.0, 10.0, 1e-6, 1000000)
+    out = [o.solve(dt * k)[2].copy() for k in range(1, nsteps + 1)]
+    nst = o.stats()["nst"]
+    oracle.OracleOde.set_reduction_order(1)
+    return out, nst
+
+
+def spread(mode, nsteps=144, dt=10.0):
+    """The problem's own divergence over the day, CPU only: the oracle chain (device reduction
+    order) against itself run with the other reduction order, and from initial states moved by one ulp (all entries
+    up, all down, three random-sign patterns).  Per variant: max / 95th percentile of the error-weighted difference
+    over the day.  The envelope (max over the variants) is what rounding-level differences alone produce; the
+    device-vs-oracle trajectory test bounds the device chain by twice it."""
+    import cases
+    _, y0 = cases.ccw()
+    ref, nref = _cpu_chain(mode, 1, y0, nsteps, dt)
+    variants = {"order0": (0, y0), "ulp_up": (1, np.nextafter(y0, np.inf)), "ulp_down": (1, np.nextafter(y0, -np.inf))}
+    for s in (1, 2, 3):
+        rng = np.random.default_rng(s)
+        variants[f"ulp_rand{s}"] = (1, np.where(rng.random(y0.size) < 0.5, np.nextafter(y0, np.inf),
+                                                np.nextafter(y0, -np.inf)))
+    out = {}
+    for name, (order, yy) in variants.items():
+        b, nb = _cpu_chain(mode, order, yy, nsteps, dt)
+        w = np.array([float(np.max(np.abs(x - y) / (1e-4 * np.abs(x) + 1e-4))) for x, y in zip(ref, b)])
+        out[name] = {"max": float(w.max()), "p95": float(np.percentile(w, 95)), "nst": [int(nref), int(nb)]}
+    out["envelope"] = {"max": max(v["max"] for v in out.values()), "p95": max(v["p95"] for v in out.values())}
+    return out
