@@ -64,6 +64,28 @@ extern "C" int shud_kat_pow(int which, const double *h_xy, int n, double *h_out)
     return rc;
 }
 
+// cos_small (shud_physics.h: OCML's small-argument cos path) next to OCML's full cos: which = 0 cos, 1 cos_small
+__global__ void kat_cos_kernel(int which, const double *__restrict__ x, int n, double *__restrict__ out) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    out[t] = which ? cos_small(x[t]) : cos(x[t]);
+}
+extern "C" int shud_kat_cos(int which, const double *h_x, int n, double *h_out) {
+    if (n <= 0) return -1;
+    double *d = nullptr;
+    const size_t bytes = sizeof(double) * (size_t)n;
+    if (hipMalloc(&d, 2 * bytes) != hipSuccess) return -3;
+    int rc = 0;
+    if (hipMemcpy(d, h_x, bytes, hipMemcpyHostToDevice) != hipSuccess) rc = -3;
+    if (!rc) {
+        hipLaunchKernelGGL(kat_cos_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, which, d, n, d + n);
+        if (hipGetLastError() != hipSuccess) rc = -3;
+    }
+    if (!rc && hipMemcpy(h_out, d + n, bytes, hipMemcpyDeviceToHost) != hipSuccess) rc = -3;
+    (void)hipFree(d);
+    return rc;
+}
+
 extern "C" int shud_kat_nin(int fn) { return (fn >= 0 && fn < KAT_COUNT) ? kat_nin_tab[fn] : -1; }
 
 extern "C" int shud_kat_eval(int fn, const double *h_in, int n, double *h_out) {

@@ -56,7 +56,8 @@ namespace shud {
 __device__ __forceinline__ double cdiv(double a, double b, double rb) {
     const double q0 = a * rb;
     const double e = __builtin_fma(-q0, b, a);
-    double q = (e == 0. || !__builtin_isfinite(e)) ? q0 : __builtin_fma(e, rb, q0);
+    // e zero, infinite or NaN (one v_cmp_class): keep q0
+    double q = __builtin_isfpclass(e, 0x0003 | 0x0204 | 0x0060) ? q0 : __builtin_fma(e, rb, q0);
     const double aa = __builtin_fabs(a);
     if (__builtin_expect((aa < 0x1p-948 && a != 0.) || aa > 0x1p1000, 0)) q = a / b;
     return q;
@@ -91,13 +92,39 @@ __device__ __forceinline__ double manning(double A, double n, double R, double S
     const double t = SDIV(SSQRT(pos ? S : -S) * A * pow23(R), n);
     return pos ? t : -t;
 }
-// Equations.cpp:116-134 (range check reported through *bad)
+// manning with the divisor's correctly rounded reciprocal (the roughness-pair table): same bits as manning
+__device__ __forceinline__ double manning_c(double A, double n, double rn, double R, double S) {
+    const bool pos = S > 0;
+    const double t = CDIV_(SSQRT(pos ? S : -S) * A * pow23(R), n, rn);
+    return pos ? t : -t;
+}
+// Equations.cpp:116-134 (range check reported by the caller).  The two macropore branches divide different
+// numerators by different divisors; the numerator and divisor are selected per branch and ONE division follows
+// the join, so a wave whose lanes take both branches runs one division sequence instead of two (same operations
+// per lane, same bits).  SHUD_EKH1=0: the branch-local divisions (A/B).
+#ifndef SHUD_EKH1
+#define SHUD_EKH1 1
+#endif
 __device__ __forceinline__ double eff_kh(double ygw, double aq, double macd, double kmac, double af,
                                          double kmx) {
     double e;
+#if SHUD_EKH1
+    if (macd <= K_ZERO || ygw < aq - macd) e = kmx;
+    else {
+        double num, den;
+        if (ygw > aq) { num = kmac * macd * af + kmx * (aq - macd * af); den = aq; }
+        else {
+            const double t = ygw - (aq - macd);
+            num = kmac * t * af + kmx * (aq - macd + t * (1 - af));
+            den = ygw;
+        }
+        e = SDIV(num, den);
+    }
+#else
     if (macd <= K_ZERO || ygw < aq - macd) e = kmx;
     else if (ygw > aq) e = SDIV(kmac * macd * af + kmx * (aq - macd * af), aq);
     else e = SDIV(kmac * (ygw - (aq - macd)) * af + kmx * (aq - macd + (ygw - (aq - macd)) * (1 - af)), ygw);
+#endif
     return e;
 }
 // MD_RiverFlux.cpp:65-98
@@ -211,9 +238,62 @@ __device__ __forceinline__ double sat_kfun(double satn, double ex1, double ex2) 
 }
 // SoilMoistureStress, is_sm_et.cpp:131-140 (truncated PI), with dth = ThetaS - ThetaR and
 // fcmr = ThetaS * 0.75 - ThetaR; b = (SatRatio * dth - ThetaR) / fcmr
+//
+// cos of K_PI * b for b in [0, 1] (the clamp also maps NaN to 0): the argument is finite and in [0, 3.1415926], so
+// OCML's cos (__ocml_cos_f64: |x|, trigred = small or Payne-Hanek reduction by |x| < 2^30, sincosred2, quadrant
+// selects, a non-finite select) reduces to its small-argument path; cos_small calls that path's own pieces in the
+// same order and returns the same bits (tests/test_kat.py::test_cos_small_bit_identical) without the large-argument
+// branch and the |x| / finiteness selects.  SHUD_COS_SMALL=0: OCML's cos (A/B).
+#ifndef SHUD_COS_SMALL
+#define SHUD_COS_SMALL 1
+#endif
+// OCML's __ocmlpriv_trigredsmall_f64 + __ocmlpriv_sincosred2_f64 (ocml.bc, ROCm 7.2) restated operation for
+// operation (their results come back in registers; a call to the bitcode's struct-returning functions went through
+// scratch and cost the kernel 48 spill instructions)
+__device__ __forceinline__ double cos_small(double x) {            // 0 <= x < 2^30, finite
+    // Cody-Waite reduction by pi/2 in three parts (trigredsmall)
+    const double q = __builtin_rint(x * 0x1.45f306dc9c883p-1);
+    const double a = __builtin_fma(q, -0x1.921fb54442d18p+0, x);
+    const double b = __builtin_fma(q, -0x1.1a62633145c00p-54, a);
+    const double p = q * 0x1.1a62633145c00p-54;
+    const double pe = __builtin_fma(q, 0x1.1a62633145c00p-54, -p);
+    const double t = a - p;
+    const double tl = ((t - b) + ((a - t) - p)) - pe;
+    const double c2 = __builtin_fma(q, -0x1.b839a252049c0p-104, tl);
+    const double hi = b + c2;
+    const double lo = c2 - (hi - b);
+    const int qi = (int)q & 3;
+    // sincosred2(hi, lo)
+    const double x2 = hi * hi;
+    const double h = x2 * 0.5;
+    const double w = 1.0 - h;
+    const double wl = (1.0 - w) - h;
+    const double x4 = x2 * x2;
+    double pc = __builtin_fma(x2, -0x1.907db46cc5e42p-37, 0x1.1eeb69037ab78p-29);
+    pc = __builtin_fma(x2, pc, -0x1.27e4fa17f65f6p-22);
+    pc = __builtin_fma(x2, pc, 0x1.a01a019f4ec90p-16);
+    pc = __builtin_fma(x2, pc, -0x1.6c16c16c16967p-10);
+    pc = __builtin_fma(x2, pc, 0x1.5555555555555p-5);
+    const double cs = w + __builtin_fma(x4, pc, __builtin_fma(hi, -lo, wl));
+    double ps = __builtin_fma(x2, 0x1.5e0b2f9a43bb8p-33, -0x1.ae600b42fdfa7p-26);
+    ps = __builtin_fma(x2, ps, 0x1.71de3796cde01p-19);
+    ps = __builtin_fma(x2, ps, -0x1.a01a019e83e5cp-13);
+    ps = __builtin_fma(x2, ps, 0x1.1111111110bb3p-7);
+    const double x3 = hi * -x2;
+    double sn = __builtin_fma(x3, ps, lo * 0.5);
+    sn = __builtin_fma(x2, sn, -lo);
+    sn = hi - __builtin_fma(x3, -0x1.5555555555555p-3, sn);
+    const double c = (qi & 1) ? -sn : cs;
+    return qi > 1 ? -c : c;
+}
+#if SHUD_COS_SMALL && !(SHUD_ABL & 2)
+#define SCOS_PI(a) cos_small(a)
+#else
+#define SCOS_PI(a) SCOS(a)
+#endif
 __device__ __forceinline__ double soil_moisture_stress(double b) {
     b = rmin(rmax(0., b), 1.);
-    return 0.5 * (1 - SCOS(K_PI * b));
+    return 0.5 * (1 - SCOS_PI(K_PI * b));
 }
 // fun_dAtodY + Quadratic, functions.hpp:125-153
 __device__ __forceinline__ double da_to_dy(double dA, double w_top, double s) {
@@ -232,7 +312,7 @@ __device__ __forceinline__ double da_to_dy(double dA, double w_top, double s) {
 // element then issue ~no atomics on the shared word, and the warning count goes to one of kWarnSlots
 // lines.  Must be reached by every active lane (it is a __ballot).
 __device__ __forceinline__ void report_w(DevErr *e, bool c, uint32_t bit, int slot, int idx, bool count = false) {
-    const unsigned long long mask = __ballot(c);
+    const unsigned long long mask = __builtin_amdgcn_ballot_w64(c);     // the compare's own lane mask
     if (mask == 0ULL) return;
     if ((int)__lane_id() == __ffsll((long long)mask) - 1) {
         if (!(__atomic_load_n(&e->flags, __ATOMIC_RELAXED) & bit)) atomicOr(&e->flags, bit);

@@ -192,6 +192,27 @@ def test_pow_pos_bit_identical():
     assert same.all(), f"{(~same).sum()} differ, first (x, y) = {xy[np.argmax(~same)]}"
 
 
+@pytest.mark.gpu
+def test_cos_small_bit_identical():
+    """cos_small (shud_physics.h: OCML's small-argument cos path without the Payne-Hanek branch and the |x| /
+    finiteness selects) returns the same bits as the device's full cos on SoilMoistureStress's arguments
+    K_PI * b, b in [0, 1] (is_sm_et.cpp:131-140), and on a wider grid below 2^30."""
+    lib = C.CDLL(os.path.join(PKG_DIR, "libshud_kat.so"))
+    lib.shud_kat_cos.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_void_p]
+    rng = np.random.default_rng(11)
+    n = 1 << 20
+    b = np.concatenate([rng.uniform(0.0, 1.0, n // 2), 10 ** rng.uniform(-17, 0, n // 4)])
+    x = np.concatenate([3.1415926 * b, rng.uniform(0.0, 2.0 ** 30, n // 8), 10 ** rng.uniform(-300, 9, n // 8),
+                        np.array([0.0, 3.1415926, np.pi / 2, np.pi / 4, np.pi, 3 * np.pi / 4, 1.0, 5e-324,
+                                  np.nextafter(2.0 ** 30, 0.0)])])
+    x = np.ascontiguousarray(x)
+    full, fast = np.zeros(x.size), np.zeros(x.size)
+    assert lib.shud_kat_cos(0, x.ctypes.data, x.size, full.ctypes.data) == 0
+    assert lib.shud_kat_cos(1, x.ctypes.data, x.size, fast.ctypes.data) == 0
+    same = full.view(np.uint64) == fast.view(np.uint64)
+    assert same.all(), f"{(~same).sum()} differ, first x = {x[np.argmax(~same)]!r}"
+
+
 def _cdiv_operands():
     """(a, b) pairs for cdiv: divisors in the handle's admitted range [2^-20, 2^20] plus 0 / inf / NaN (the
     class constants a model may carry), numerators across the whole double range with the guard boundaries
