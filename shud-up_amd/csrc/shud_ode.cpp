@@ -39,6 +39,12 @@ constexpr double ADDON = 0.000001, BIAS1 = 6.0, BIAS2 = 6.0, BIAS3 = 10.0, ONEPS
 constexpr int SMALL_NST = 10, MXNCF = 10, MXNEF = 7, MXNEF1 = 3, SMALL_NEF = 2, LONG_WAIT = 10, MSBP = 20;
 constexpr double DGMAX = 0.3, CRDOWN = 0.3, RDIV = 2.0, NLSCOEF = 0.1;
 constexpr int NLS_MAXCOR = 3;
+// SHUD_ODE_LAZY_COMPLETE=0: cvCompleteStep updates all of zn[0..q] in its own pass (A/B); default: zn[0] at once,
+// zn[1..q] deferred into the next predict (ode::Pend)
+#ifndef SHUD_ODE_LAZY_COMPLETE
+#define SHUD_ODE_LAZY_COMPLETE 1
+#endif
+constexpr bool kLazyComplete = SHUD_ODE_LAZY_COMPLETE != 0;
 constexpr double CVLS_EPLIN = 0.05, CVLS_DGMAX = 0.2;
 constexpr int CVLS_MSBJ = 51;
 enum { FIRST_CALL = 0, PREV_CONV_FAIL = 1, PREV_ERR_FAIL = 2 };
@@ -190,15 +196,30 @@ struct shud_ode {
     // not stored, acor_lazy), which the cvNls start that always follows it would otherwise do in a separate pass
     // (k_vsum_zero)
     bool y_pred = false;
+    // the last step's cvCompleteStep on zn[1..q] (+ zn[qmax] = acor) and a following cvRescale, deferred into the
+    // next pass that reads zn[1..q] (ode::Pend; zn[0] is completed at once by complete_step_ewt)
+    ode::Pend pend{};
+    void materialize() {                                             // apply a deferred completion now
+        if (!pend.acor) return;
+        complete_step(n, zn, pend.acor, pend.l, 1, pend.q, pend.copy_to, s);
+        if (pend.resc) ode::rescale(n, zn, pend.q, pend.r, s);
+        pend = ode::Pend{};
+    }
     void predict() {
         tn += h;
         if (tstopset && (tn - tstop) * h > 0.0) tn = tstop;
-        ode::predict(n, zn, q, y, acor, s);
+        if (pend.acor && pend.q == q) ode::predict_pend(n, zn, q, y, acor, pend, s);
+        else {
+            materialize();
+            ode::predict(n, zn, q, y, acor, s);
+        }
+        pend = ode::Pend{};
         y_pred = true;
         acor_lazy = ode::lazy_ycor() != 0;
     }
     void restore(double saved_t) {
         tn = saved_t;
+        materialize();                // (never pending here: a restore follows a predict)
         ode::restore(n, zn, q, s);
         y_pred = false;               // (acor_lazy kept: a failed attempt's acor is still logically +0.0)
     }
@@ -206,7 +227,13 @@ struct shud_ode {
         Coefs c{};
         double x = eta;
         for (int j = 1; j <= q; ++j) { c.c[j] = x; x = eta * x; }
-        ode::rescale(n, zn, q, c, s);
+        if (pend.acor && !pend.resc && pend.q == q) {                 // after a deferred completion: fused too
+            pend.r = c;
+            pend.resc = 1;
+        } else {
+            materialize();
+            ode::rescale(n, zn, q, c, s);
+        }
         h = hscale * eta;
         next_h = h;
         hscale = h;
@@ -257,6 +284,7 @@ struct shud_ode {
     }
     void adjust_params() {
         if (qprime != q) {
+            materialize();                                           // cvAdjustOrder reads zn[2..q] and zn[qmax]
             adjust_order(qprime - q);
             q = qprime;
             L = q + 1;
@@ -544,8 +572,18 @@ struct shud_ode {
             saved_tq5 = tq[5];
             indx_acor = qmax;
         }
-        // cvCompleteStep + the next loop iteration's cvEwtSet / N_VWrmsNorm(zn[0]) in one pass (ewt_and_norm)
-        complete_step_ewt(n, zn, acor, lc, q, copy_to, rtol, atol, ewt_alt, rs(S_EWTMIN), s);
+        // cvCompleteStep + the next loop iteration's cvEwtSet / N_VWrmsNorm(zn[0]) in one pass (ewt_and_norm);
+        // SHUD_ODE_LAZY_COMPLETE: that pass completes zn[0] only, zn[1..q] and the acor copy ride in the next predict
+        if (kLazyComplete) {
+            complete_step_ewt(n, zn, acor, lc, 0, -1, rtol, atol, ewt_alt, rs(S_EWTMIN), s);
+            pend = ode::Pend{};
+            pend.acor = acor;
+            pend.l = lc;
+            pend.q = q;
+            pend.copy_to = copy_to;
+        } else {
+            complete_step_ewt(n, zn, acor, lc, q, copy_to, rtol, atol, ewt_alt, rs(S_EWTMIN), s);
+        }
         finalize(rs(S_EWTMIN), 2, 1u, s);
         ewt_pending = true;
         ewt_fin_sync = n_sync;
@@ -571,7 +609,9 @@ struct shud_ode {
         double cquot = 0.0;
         if (qp1) cquot = (tq[5] / saved_tq5) * rpower_i(h / tau[2], L);
         if (qm1 || qp1) {
-            eta_norms(n, qm1 ? Z(q) : nullptr, qp1 ? Z(qmax) : nullptr, acor, -cquot, ewt, rs(S_ETAQM1), s);
+            const bool pq = qm1 && pend.acor && q >= 1 && q <= pend.q;
+            eta_norms(n, qm1 ? Z(q) : nullptr, qp1 ? Z(qmax) : nullptr, acor, -cquot, ewt, pq ? 1 : 0,
+                      pq ? pend.l.c[q] : 0.0, rs(S_ETAQM1), s);
             finalize(rs(S_ETAQM1), 2, 0u, s);
             if (!fetch()) return -1;
         }
@@ -596,7 +636,7 @@ struct shud_ode {
         } else {
             eta = etaqp1;
             qprime = q + 1;
-            copy(n, acor, Z(qmax), s);
+            copy(n, acor, Z(qmax), s);     // (a pending completion has copy_to < 0 here: qwait was 0, not 1)
         }
         set_eta();
         return 0;
@@ -641,7 +681,7 @@ struct shud_ode {
             js[nvec] = j;
             nvec++;
         }
-        ode::dky(n, zn, n, js, c, nvec, k == 0 ? 0.0 : rpower_i(h, -k), out, s);
+        ode::dky(n, zn, n, js, c, nvec, k == 0 ? 0.0 : rpower_i(h, -k), out, pend, s);
         return SHUD_ODE_SUCCESS;
     }
     int ewt_and_norm() {                                              // cvEwtSet + N_VWrmsNorm(zn[0])

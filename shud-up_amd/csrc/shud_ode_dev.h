@@ -56,6 +56,16 @@ struct Coefs {         // small host-computed coefficient arrays passed by value
     double c[kMaxL + 1];
 };
 
+// A deferred cvCompleteStep on zn[1..q] (zn[j] = l[j]*acor + zn[j]) and its zn[copy_to] = acor, and a deferred
+// cvRescale after it (zn[j] *= r[j], j = 1..q): applied in registers by the first pass that reads zn[1..q] (the
+// next cvPredict, a CVodeGetDky, cvComputeEtaqm1's norm), or materialized before an order change.  zn[0] is always
+// completed at once (the ewt pass needs it).  acor == nullptr: nothing pending.
+struct Pend {
+    const double *acor;
+    Coefs l, r;
+    int q, copy_to, resc;
+};
+
 // ---- launchers (hipStream_t s); a reduction kernel leaves per-block partials, finalize(r, nacc, minmask) writes
 // its nacc results to slots [r.slot0, r.slot0 + nacc) ----
 void finalize(const Red &r, int nacc, unsigned minmask, hipStream_t s);
@@ -63,6 +73,8 @@ void finalize(const Red &r, int nacc, unsigned minmask, hipStream_t s);
 void ewt_set(int64_t n, const double *zn0, double *ewt, double rtol, double atol, const Red &r, hipStream_t s);
 // cvPredict; with y/ycor != null also ycor = 0 and y = zn[0] + 0.0 (the following cvNls start)
 void predict(int64_t n, double *zn, int q, double *y, double *ycor, hipStream_t s);
+// predict with a pending complete (+ rescale) applied first: pd.q == q, pd.acor != null
+void predict_pend(int64_t n, double *zn, int q, double *y, double *ycor, const Pend &pd, hipStream_t s);
 void restore(int64_t n, double *zn, int q, hipStream_t s);
 void rescale(int64_t n, double *zn, int q, const Coefs &c, hipStream_t s);
 void vsum(int64_t n, const double *x, const double *y, double *z, hipStream_t s);
@@ -95,17 +107,20 @@ void newton_update(int64_t n, const double *V, int64_t vstride, int krydim, cons
 // 1 when predict() leaves ycor unwritten (SHUD_ODE_LAZY_YCOR): the caller then passes ycor_zero until the first
 // newton_update after a predict
 int lazy_ycor();
-// zn[j] = l[j]*acor + zn[j], j = 0..q; if copy_to >= 0: zn[copy_to] = acor
-void complete_step(int64_t n, double *zn, const double *acor, const Coefs &l, int q, int copy_to, hipStream_t s);
+// zn[j] = l[j]*acor + zn[j], j = jlo..q; if copy_to >= 0: zn[copy_to] = acor
+void complete_step(int64_t n, double *zn, const double *acor, const Coefs &l, int jlo, int q, int copy_to,
+                   hipStream_t s);
 // complete_step, then ewt_set's arithmetic on the new zn[0] into ewt_next; r: [min(rtol|y| + atol), sum (y*w)^2]
 void complete_step_ewt(int64_t n, double *zn, const double *acor, const Coefs &l, int q, int copy_to, double rtol,
                        double atol, double *ewt_next, const Red &r, hipStream_t s);
-// r: [sum (zn_q*ewt)^2 (zn_q != NULL), sum (((-cquot)*zn_qmax + acor)*ewt)^2 (zn_qmax != NULL)]
+// r: [sum (zn_q*ewt)^2 (zn_q != NULL), sum (((-cquot)*zn_qmax + acor)*ewt)^2 (zn_qmax != NULL)]; pend_q: zn_q's
+// completion is pending, zn_q = lq*acor + zn_q on the fly
 void eta_norms(int64_t n, const double *zn_q, const double *zn_qmax, const double *acor, double ncquot,
-               const double *ewt, const Red &r, hipStream_t s);
-// dky = lincomb(c, zn[js]) (N_VLinearCombination), then dky *= rscale if rscale != 0
+               const double *ewt, int pend_q, double lq, const Red &r, hipStream_t s);
+// dky = lincomb(c, zn[js]) (N_VLinearCombination), then dky *= rscale if rscale != 0; zn[j] with a pending
+// completion (pd.acor, 1 <= j <= pd.q) taken on the fly
 void dky(int64_t n, const double *zn, int64_t stride, const int *js, const Coefs &c, int nvec, double rscale,
-         double *out, hipStream_t s);
+         double *out, const Pend &pd, hipStream_t s);
 int grid_blocks(int64_t n);
 
 }  // namespace ode

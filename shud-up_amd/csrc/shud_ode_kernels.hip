@@ -186,22 +186,38 @@ void ewt_set(int64_t n, const double *zn0, double *ewt, double rtol, double atol
 // SHUD_ODE_LAZY_YCOR (default): the ycor = 0 fill is not stored at all — the controller marks ycor "all +0.0"
 // and its only readers before the first Newton update (k_residual, k_newton_update) take the zeros as operands
 // instead of loading them (identical values; -8 B/entry here and in that k_newton_update)
-template <int Q, bool FWD, int U>
+// PEND (cvPredict after a deferred cvCompleteStep, Pend): zn[j] = l[j]*acor + zn[j] and zn[j] *= r[j] (j = 1..Q) in
+// registers first — k_complete's and k_rescale's arithmetic — then the Pascal update; zn[Q] is stored too, and
+// zn[copy_to] = acor.  Saves the completion's own pass over zn[1..Q] (+16 B/entry here, -16*Q B/entry there).
+template <int Q, bool FWD, bool PEND, int U>
 __global__ void __launch_bounds__(kThreads) k_pascal(int64_t n, double *__restrict__ zn, double *__restrict__ y,
-                                                     double *__restrict__ ycor) {
-    using T = DN<Q + 1>;
+                                                     double *__restrict__ ycor, Pend pd) {
+    using T = DN<Q + 2>;                  // [0..Q] zn, [Q + 1] acor (PEND)
     one<T>(n, [&](int64_t i) {
         T a;
 #pragma unroll
         for (int j = 0; j <= Q; ++j) a.v[j] = ldn(zn + (int64_t)j * n + i);
+        a.v[Q + 1] = PEND ? ldn(pd.acor + i) : 0.0;
         return a;
     }, [&](int64_t i, T a) {
+        if (PEND) {
+#pragma unroll
+            for (int j = 1; j <= Q; ++j) a.v[j] = pd.l.c[j] * a.v[Q + 1] + a.v[j];
+            if (pd.resc) {
+#pragma unroll
+                for (int j = 1; j <= Q; ++j) a.v[j] = a.v[j] * pd.r.c[j];
+            }
+        }
 #pragma unroll
         for (int k = 1; k <= Q; ++k)
 #pragma unroll
             for (int j = Q; j >= k; --j) a.v[j - 1] = FWD ? a.v[j - 1] + a.v[j] : a.v[j - 1] - a.v[j];
 #pragma unroll
         for (int j = 0; j < Q; ++j) stn(zn + (int64_t)j * n + i, a.v[j]);
+        if (PEND) {
+            stn(zn + (int64_t)Q * n + i, a.v[Q]);
+            if (pd.copy_to >= 0) stn(zn + (int64_t)pd.copy_to * n + i, a.v[Q + 1]);
+        }
         if (FWD && y) {
             const double zero = 0.0;
             if (SHUD_ODE_LAZY_YCOR == 0) stn(ycor + i, zero);
@@ -209,25 +225,28 @@ __global__ void __launch_bounds__(kThreads) k_pascal(int64_t n, double *__restri
         }
     });
 }
-template <int Q, bool FWD>
-static void pascal_q(int64_t n, double *zn, double *y, double *ycor, hipStream_t s) {
-    k_pascal<Q, FWD, 1><<<ew_blocks(n), kThreads, 0, s>>>(n, zn, y, ycor);
+template <int Q, bool FWD, bool PEND>
+static void pascal_q(int64_t n, double *zn, double *y, double *ycor, const Pend &pd, hipStream_t s) {
+    k_pascal<Q, FWD, PEND, 1><<<ew_blocks(n), kThreads, 0, s>>>(n, zn, y, ycor, pd);
 }
-template <bool FWD>
-static void pascal(int64_t n, double *zn, int q, double *y, double *ycor, hipStream_t s) {
+template <bool FWD, bool PEND>
+static void pascal(int64_t n, double *zn, int q, double *y, double *ycor, const Pend &pd, hipStream_t s) {
     switch (q) {
-    case 1: pascal_q<1, FWD>(n, zn, y, ycor, s); break;
-    case 2: pascal_q<2, FWD>(n, zn, y, ycor, s); break;
-    case 3: pascal_q<3, FWD>(n, zn, y, ycor, s); break;
-    case 4: pascal_q<4, FWD>(n, zn, y, ycor, s); break;
-    default: pascal_q<5, FWD>(n, zn, y, ycor, s); break;
+    case 1: pascal_q<1, FWD, PEND>(n, zn, y, ycor, pd, s); break;
+    case 2: pascal_q<2, FWD, PEND>(n, zn, y, ycor, pd, s); break;
+    case 3: pascal_q<3, FWD, PEND>(n, zn, y, ycor, pd, s); break;
+    case 4: pascal_q<4, FWD, PEND>(n, zn, y, ycor, pd, s); break;
+    default: pascal_q<5, FWD, PEND>(n, zn, y, ycor, pd, s); break;
     }
 }
 int lazy_ycor() { return SHUD_ODE_LAZY_YCOR; }
 void predict(int64_t n, double *zn, int q, double *y, double *ycor, hipStream_t s) {
-    pascal<true>(n, zn, q, y, ycor, s);
+    pascal<true, false>(n, zn, q, y, ycor, Pend{}, s);
 }
-void restore(int64_t n, double *zn, int q, hipStream_t s) { pascal<false>(n, zn, q, nullptr, nullptr, s); }
+void predict_pend(int64_t n, double *zn, int q, double *y, double *ycor, const Pend &pd, hipStream_t s) {
+    pascal<true, true>(n, zn, q, y, ycor, pd, s);
+}
+void restore(int64_t n, double *zn, int q, hipStream_t s) { pascal<false, false>(n, zn, q, nullptr, nullptr, Pend{}, s); }
 
 // cvRescale: zn[j] *= eta^j (N_VScaleVectorArray).  16*q B/entry.
 template <int U>
@@ -491,27 +510,29 @@ void newton_update(int64_t n, const double *V, int64_t vstride, int krydim, cons
     LAUNCH_RED(k_newton_update, r, s, n, V, vstride, krydim, yg, dsrc, ewt, ycor, (int)ycor_zero);
 }
 
-// cvCompleteStep: zn[j] = l[j]*acor + zn[j] (N_VScaleAddMulti), optional zn[qmax] = acor.
+// cvCompleteStep: zn[j] = l[j]*acor + zn[j] (N_VScaleAddMulti) for j in [jlo, q], optional zn[qmax] = acor.
 template <int U>
 __global__ void __launch_bounds__(kThreads) k_complete(int64_t n, double *__restrict__ zn,
-                                                       const double *__restrict__ acor, Coefs l, int q, int copy_to) {
-    using T = DN<kQMax + 2>;              // [0] acor, [1 + j] zn[j], j <= q
+                                                       const double *__restrict__ acor, Coefs l, int jlo, int q,
+                                                       int copy_to) {
+    using T = DN<kQMax + 2>;              // [0] acor, [1 + j] zn[j], jlo <= j <= q
     one<T>(n, [&](int64_t i) {
         T a;
         a.v[0] = ldn(acor + i);
 #pragma unroll
         for (int j = 0; j <= kQMax; ++j)
-            if (j <= q) a.v[1 + j] = ldn(zn + (int64_t)j * n + i);
+            if (j >= jlo && j <= q) a.v[1 + j] = ldn(zn + (int64_t)j * n + i);
         return a;
     }, [&](int64_t i, const T &a) {
 #pragma unroll
         for (int j = 0; j <= kQMax; ++j)
-            if (j <= q) stn(zn + (int64_t)j * n + i, l.c[j] * a.v[0] + a.v[1 + j]);
+            if (j >= jlo && j <= q) stn(zn + (int64_t)j * n + i, l.c[j] * a.v[0] + a.v[1 + j]);
         if (copy_to >= 0) stn(zn + (int64_t)copy_to * n + i, a.v[0]);
     });
 }
-void complete_step(int64_t n, double *zn, const double *acor, const Coefs &l, int q, int copy_to, hipStream_t s) {
-    LAUNCH_EW(k_complete, n, s, zn, acor, l, q, copy_to);
+void complete_step(int64_t n, double *zn, const double *acor, const Coefs &l, int jlo, int q, int copy_to,
+                   hipStream_t s) {
+    LAUNCH_EW(k_complete, n, s, zn, acor, l, jlo, q, copy_to);
 }
 
 // cvCompleteStep fused with the next step's cvEwtSetSS + N_VWrmsNorm(zn[0], ewt) (CVode's loop runs them back to
@@ -560,14 +581,16 @@ template <int U>
 __global__ void __launch_bounds__(kRedThreads) k_eta_norms(int64_t n, const double *__restrict__ znq,
                                                         const double *__restrict__ znqmax,
                                                         const double *__restrict__ acor, double ncquot,
-                                                        const double *__restrict__ ewt, Red r) {
+                                                        const double *__restrict__ ewt, int pq, double lq, Red r) {
     double v[2] = {0.0, 0.0};
+    const bool need_acor = znqmax || pq;
     one<D4>(n, [&](int64_t i) {
-        return D4{ldn(ewt + i), znq ? ldn(znq + i) : 0.0, znqmax ? ldn(znqmax + i) : 0.0, znqmax ? ldn(acor + i) : 0.0};
+        return D4{ldn(ewt + i), znq ? ldn(znq + i) : 0.0, znqmax ? ldn(znqmax + i) : 0.0, need_acor ? ldn(acor + i) : 0.0};
     }, [&](int64_t, const D4 &o) {
         const double e = o.a;
         if (znq) {
-            const double p = o.b * e;
+            const double zq = pq ? lq * o.d + o.b : o.b;              // pending completion: k_complete's value
+            const double p = zq * e;
             v[0] += p * p;
         }
         if (znqmax) {
@@ -579,8 +602,8 @@ __global__ void __launch_bounds__(kRedThreads) k_eta_norms(int64_t n, const doub
     block_partial<2>(v, 0u, r);
 }
 void eta_norms(int64_t n, const double *zn_q, const double *zn_qmax, const double *acor, double ncquot,
-               const double *ewt, const Red &r, hipStream_t s) {
-    LAUNCH_RED(k_eta_norms, r, s, n, zn_q, zn_qmax, acor, ncquot, ewt);
+               const double *ewt, int pend_q, double lq, const Red &r, hipStream_t s) {
+    LAUNCH_RED(k_eta_norms, r, s, n, zn_q, zn_qmax, acor, ncquot, ewt, pend_q, lq);
 }
 
 // N_VLinearSum_Serial's case analysis for z distinct from x and y
@@ -603,26 +626,31 @@ struct Js {
 
 // CVodeGetDky: N_VLinearCombination(nvec, c, zn[js], dky), then N_VScale(h^-k, dky, dky) for k > 0
 __global__ void __launch_bounds__(kThreads) k_dky(int64_t n, const double *__restrict__ zn, int64_t stride, Js js,
-                                                  Coefs c, int nvec, double rscale, double *__restrict__ out) {
+                                                  Coefs c, int nvec, double rscale, double *__restrict__ out, Pend pd) {
     for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
+        const double ac = pd.acor ? pd.acor[i] : 0.0;
+        auto Zj = [&](int j) {            // zn[j] as completed (k_complete's value when its completion is pending)
+            const double z = zn[j * stride + i];
+            return (pd.acor && j >= 1 && j <= pd.q) ? pd.l.c[j] * ac + z : z;
+        };
         double z;
         if (nvec == 1) {
-            z = c.c[0] * zn[js.j[0] * stride + i];
+            z = c.c[0] * Zj(js.j[0]);
         } else if (nvec == 2) {
-            z = lin_sum2(c.c[0], zn[js.j[0] * stride + i], c.c[1], zn[js.j[1] * stride + i]);
+            z = lin_sum2(c.c[0], Zj(js.j[0]), c.c[1], Zj(js.j[1]));
         } else {
-            z = c.c[0] * zn[js.j[0] * stride + i];
-            for (int k = 1; k < nvec; ++k) z += c.c[k] * zn[js.j[k] * stride + i];
+            z = c.c[0] * Zj(js.j[0]);
+            for (int k = 1; k < nvec; ++k) z += c.c[k] * Zj(js.j[k]);
         }
         if (rscale != 0.0) z *= rscale;
         out[i] = z;
     }
 }
 void dky(int64_t n, const double *zn, int64_t stride, const int *jsv, const Coefs &c, int nvec, double rscale,
-         double *out, hipStream_t s) {
+         double *out, const Pend &pd, hipStream_t s) {
     Js js{};
     for (int k = 0; k < nvec && k <= kQMax; ++k) js.j[k] = jsv[k];
-    k_dky<<<ew_blocks(n), kThreads, 0, s>>>(n, zn, stride, js, c, nvec, rscale, out);   // one entry per thread
+    k_dky<<<ew_blocks(n), kThreads, 0, s>>>(n, zn, stride, js, c, nvec, rscale, out, pd);   // one entry per thread
 }
 
 }  // namespace ode

@@ -1,6 +1,6 @@
 #!/bin/bash
 # build an A/B variant of libshud_rhs.so with extra -D flags for one translation unit (default: the packed element
-# kernel, shud_ele_packed.hip; -tu ode: the integrator kernels, shud_ode_kernels.hip; -tu rhs: the runtime, shud_rhs.cpp):
+# kernel, shud_ele_packed.hip; -tu ode: the integrator kernels, shud_ode_kernels.hip; -tu rhs: the runtime, shud_rhs.cpp; -tu odehost: the integrator controller, shud_ode.cpp):
 #   tools/ablib.sh NAME [-tu ode] -DFOO=1 ...   ->  shud-up_amd/build/ab/libshud_rhs_NAME.so
 set -e
 cd "$(dirname "$0")/../shud-up_amd"
@@ -11,6 +11,7 @@ if [ "$1" = "-tu" ]; then
     ode) src=csrc/shud_ode_kernels.hip; obj=shud_ode_kernels.o ;;
     ele) ;;
     rhs) src=csrc/shud_rhs.cpp; obj=shud_rhs.o ;;
+    odehost) src=csrc/shud_ode.cpp; obj=shud_ode.o ;;
     *) echo "unknown TU $2"; exit 2 ;;
   esac
   shift 2
