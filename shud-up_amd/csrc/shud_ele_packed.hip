@@ -669,6 +669,10 @@ __device__ __forceinline__ double riv_down_outlet(const RivP &q, double uq, cons
 #ifndef SHUD_RIV_ABL
 #define SHUD_RIV_ABL 0
 #endif
+// SHUD_RIV_SEGMASK: segment gathers masked to each reach's own segments (A/B; 0: clamped to the first segment)
+#ifndef SHUD_RIV_SEGMASK
+#define SHUD_RIV_SEGMASK 0
+#endif
 // SHUD_RIV_V: 1 = one chain per neighbour (production), 2 = dependence-ordered loads (A/B)
 #ifndef SHUD_RIV_V
 #define SHUD_RIV_V 1
@@ -842,11 +846,20 @@ shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     } else
     for (int k0 = ii.z, k1 = ii.z + ii.w; k0 < k1; k0 += 8) {
         int ps[8];
+        double2 qv[8];
+#if SHUD_RIV_SEGMASK
+        // lanes past their reach's last segment issue no request (a divergent gather costs the address unit one
+        // request per active lane, whatever line it hits)
+#pragma unroll
+        for (int j = 0; j < 8; j++) ps[j] = k0 + j < k1 ? m.rseg_pos[k0 + j] : 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) qv[j] = k0 + j < k1 ? p.qseg2[ps[j]] : make_double2(0., 0.);
+#else
 #pragma unroll
         for (int j = 0; j < 8; j++) ps[j] = m.rseg_pos[k0 + j < k1 ? k0 + j : k0];
-        double2 qv[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) qv[j] = p.qseg2[ps[j]];
+#endif
 #pragma unroll
         for (int j = 0; j < 8; j++)
             if (k0 + j < k1) { qsurf += qv[j].x; qsub += qv[j].y; }
