@@ -51,6 +51,45 @@ __global__ void __launch_bounds__(256, 5) k_prod(Prod P, int ne, int row, int pe
     __builtin_nontemporal_store(acc * 4., P.dy + 2 * (size_t)ne + i);
 }
 
+// the production skeleton plus synthetic fp64 VALU work (NV dependent FMAs in 4 independent chains: ~60 % after
+// the own record, the rest spread over the edge iterations) — how much VALU the access pattern hides
+__device__ __forceinline__ void burn(double (&c)[4], int n) {
+    for (int k = 0; k < n; k++) {
+#pragma unroll
+        for (int t = 0; t < 4; t++) c[t] = __builtin_fma(c[t], 1.0000001, 1e-9);
+    }
+}
+__global__ void __launch_bounds__(256, 5) k_prod_v(Prod P, int ne, int row, int per8, int nv) {
+    extern __shared__ double pad[];
+    const int i = tile_of(per8) * 256 + (int)threadIdx.x;
+    if (i >= ne) return;
+    const v4i mt = P.meta[i];
+    const v2d zz = P.zz[i];
+    const double ys = P.y[i], yu = P.y[ne + i], yg = P.y[2 * (size_t)ne + i];
+    const v2d snp = ldnt(P.snp + i), stl = ldnt(P.stl + i), csv = ldnt(P.csv + i);
+    const int sfl = P.sfl[i];
+    const double area = __builtin_nontemporal_load(P.area + i);
+    double c[4] = {zz.x + ys, zz.y + yu, yg + snp.x + snp.y, stl.x + stl.y + csv.x + csv.y + sfl + mt.w};
+    burn(c, (nv * 3 / 5) / 4);
+    double acc = c[0] + c[1] + c[2] + c[3];
+    for (int j = 0; j < 3; j++) {
+        const int nb = nbr(i, j, ne, row);
+        const int nc = nb >= 0 ? nb : i;
+        const v2d g = ldnt(P.ged + (size_t)j * ne + i);
+        const v2d nz = P.zz[nc];
+        const int ncf = ((const int *)(P.meta + nc))[3];
+        double d[4] = {g.x * g.y + acc, nz.x + nz.y, ncf + P.y[nc], P.y[2 * (size_t)ne + nc]};
+        burn(d, (nv * 2 / 15) / 4);
+        acc += d[0] + d[1] + d[2] + d[3];
+    }
+    if (acc == 1234.5) pad[threadIdx.x] = acc;
+    v2d o; o.x = acc; o.y = area;
+    __builtin_nontemporal_store(o, P.cs + i);
+    __builtin_nontemporal_store(acc * 2., P.dy + i);
+    __builtin_nontemporal_store(acc * 3., P.dy + ne + i);
+    __builtin_nontemporal_store(acc * 4., P.dy + 2 * (size_t)ne + i);
+}
+
 // record layout: one 128-B line per element {meta | zz | snp | stl | ged0 | ged1 | ged2 | area, sfl, pad}; y and dy
 // stay the ABI's blocks, the carried state its ping-pong pair
 struct Rec {
@@ -116,6 +155,14 @@ int main(int argc, char **argv) {
     const double tp = timeit([&] { hipLaunchKernelGGL(k_prod, dim3(nb), dim3(256), 0, 0, P, ne, row, nb / 8); }, 50);
     const double tr = timeit([&] { hipLaunchKernelGGL(k_rec, dim3(nb), dim3(256), 0, 0, R, ne, row, nb / 8); }, 50);
     const double bp = (double)ne * (164 + 40), br = (double)ne * (168 + 40);
+    // synthetic VALU per element nv (the element kernel issues ~1,380 VALU per wave = per element), LDS padding to
+    // hold 6 (lds 26 KiB) or 5 workgroups per CU like the element kernel
+    for (int lds : {0, 26 * 1024}) {
+        for (int nv : {0, 400, 800, 1200, 1600}) {
+            const double tv = timeit([&] { hipLaunchKernelGGL(k_prod_v, dim3(nb), dim3(256), lds, 0, P, ne, row, nb / 8, nv); }, 30);
+            printf("{\"num_ele\": %d, \"lds\": %d, \"valu_per_element\": %d, \"ms\": %.4f}\n", ne, lds, nv, tv);
+        }
+    }
     printf("{\"num_ele\": %d, \"prod_ms\": %.4f, \"prod_GBs_unique\": %.0f, \"rec_ms\": %.4f, \"rec_GBs_unique\": %.0f}\n", ne,
            tp, bp / tp / 1e6, tr, br / tr / 1e6);
     return 0;

@@ -21,8 +21,8 @@ PER_ENTRY = {
     "k_mgs": lambda q: 32,               # w, Vprev, Vnext, w (the last pass of an iteration moves 24)
     "k_normalize": lambda q: 24,
     "k_newton_update": lambda q: 8 * (3 + 2),   # ewt, ycor, ~2 Krylov vectors, ycor
-    "k_complete": lambda q: 8 * (1 + 2 * (q + 1)),
-    "k_complete_ewt": lambda q: 8 * (1 + 2 * (q + 1)) + 8,   # + the next step's ewt (round 3)
+    "k_complete": lambda q: 8 * (1 + 2 * q),                # round 4: materializes zn[1..q] (eager: 1 + 2(q+1))
+    "k_complete_ewt": lambda q: 32,         # round 4: acor, zn[0] -> zn[0], ewt (eager: 8 * (1 + 2(q+1)) + 8)
     "k_rescale": lambda q: 16 * q,
     "k_eta_norms": lambda q: 32,
 }
@@ -34,6 +34,8 @@ def main():
     ap.add_argument("ny", type=int)
     ap.add_argument("--q", type=int, default=3)
     ap.add_argument("--eager-ycor", action="store_true", help="sources before the lazy ycor (predict stores ycor = 0)")
+    ap.add_argument("--eager-complete", action="store_true",
+                    help="sources before round 4's deferred cvCompleteStep (complete_ewt updates all of zn)")
     ap.add_argument("--copy-gbs", type=float, default=6400.0, help="the box's STREAM copy rate")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.csv)))
@@ -43,15 +45,22 @@ def main():
         name = r["Name"]
         m = re.search(r"(k_\w+?)(?:<|\(|I)", name.replace("shud::ode::", ""))
         if "pascal" in name:
-            mm = re.search(r"k_pascal<(\d), (true|false)", name)
+            mm = re.search(r"k_pascal<(\d), (true|false)(?:, (true|false))?", name)
             q = int(mm.group(1))
             fwd = mm.group(2) == "true"
+            pend = mm.group(3) == "true"
             lazy = "--eager-ycor" not in sys.argv
             b = 8 * (2 * q + 1) + ((8 if lazy else 16) if fwd else 0)   # predict also writes y (+ ycor unless lazy)
-            key = f"k_pascal<{q},{'pred' if fwd else 'rest'}>"
+            if pend:
+                b += 16                         # the deferred completion: acor in, zn[q] out
+            key = f"k_pascal<{q},{'pend' if pend else 'pred' if fwd else 'rest'}>"
         elif m and m.group(1) in PER_ENTRY:
             key = m.group(1)
             b = PER_ENTRY[key](a.q)
+            if a.eager_complete and key == "k_complete":
+                b = 8 * (1 + 2 * (a.q + 1))
+            if a.eager_complete and key == "k_complete_ewt":
+                b = 8 * (1 + 2 * (a.q + 1)) + 8
         elif "k_finalize" in name:
             key, b = "k_finalize", 0
         else:
