@@ -90,6 +90,50 @@ __global__ void __launch_bounds__(256, 5) k_prod_v(Prod P, int ne, int row, int 
     __builtin_nontemporal_store(acc * 4., P.dy + 2 * (size_t)ne + i);
 }
 
+// two tiles per workgroup: the second tile's own streams are loaded while the first tile computes (software
+// prefetch into registers) — does a wave that always has loads in flight fix the few-rounds case?
+struct Own { v4i mt; v2d zz, snp, stl, csv; double ys, yu, yg, area; int sfl; };
+__device__ __forceinline__ Own own_load(const Prod &P, int ne, int i) {
+    Own o;
+    o.mt = P.meta[i]; o.zz = P.zz[i];
+    o.ys = P.y[i]; o.yu = P.y[ne + i]; o.yg = P.y[2 * (size_t)ne + i];
+    o.snp = ldnt(P.snp + i); o.stl = ldnt(P.stl + i); o.csv = ldnt(P.csv + i);
+    o.sfl = P.sfl[i]; o.area = __builtin_nontemporal_load(P.area + i);
+    return o;
+}
+__device__ __forceinline__ void own_body(const Prod &P, int ne, int row, int i, const Own &o, int nv) {
+    double c[4] = {o.zz.x + o.ys, o.zz.y + o.yu, o.yg + o.snp.x + o.snp.y,
+                   o.stl.x + o.stl.y + o.csv.x + o.csv.y + o.sfl + o.mt.w};
+    burn(c, (nv * 3 / 5) / 4);
+    double acc = c[0] + c[1] + c[2] + c[3];
+    for (int j = 0; j < 3; j++) {
+        const int nb = nbr(i, j, ne, row);
+        const int nc = nb >= 0 ? nb : i;
+        const v2d g = ldnt(P.ged + (size_t)j * ne + i);
+        const v2d nz = P.zz[nc];
+        const int ncf = ((const int *)(P.meta + nc))[3];
+        double d[4] = {g.x * g.y + acc, nz.x + nz.y, ncf + P.y[nc], P.y[2 * (size_t)ne + nc]};
+        burn(d, (nv * 2 / 15) / 4);
+        acc += d[0] + d[1] + d[2] + d[3];
+    }
+    v2d ov; ov.x = acc; ov.y = o.area;
+    __builtin_nontemporal_store(ov, P.cs + i);
+    __builtin_nontemporal_store(acc * 2., P.dy + i);
+    __builtin_nontemporal_store(acc * 3., P.dy + ne + i);
+    __builtin_nontemporal_store(acc * 4., P.dy + 2 * (size_t)ne + i);
+}
+__global__ void __launch_bounds__(256, 4) k_prod_2t(Prod P, int ne, int row, int per8, int nv, int half) {
+    extern __shared__ double pad[];
+    const int t0 = tile_of(per8);
+    const int ia = t0 * 256 + (int)threadIdx.x, ib = (t0 + half) * 256 + (int)threadIdx.x;
+    Own a, b;
+    if (ia < ne) a = own_load(P, ne, ia);
+    if (ib < ne) b = own_load(P, ne, ib);
+    if (ia < ne) own_body(P, ne, row, ia, a, nv);
+    if (ib < ne) own_body(P, ne, row, ib, b, nv);
+    if (nv == -1) pad[threadIdx.x] = 0.;
+}
+
 // record layout: one 128-B line per element {meta | zz | snp | stl | ged0 | ged1 | ged2 | area, sfl, pad}; y and dy
 // stay the ABI's blocks, the carried state its ping-pong pair
 struct Rec {
@@ -157,6 +201,14 @@ int main(int argc, char **argv) {
     const double bp = (double)ne * (164 + 40), br = (double)ne * (168 + 40);
     // synthetic VALU per element nv (the element kernel issues ~1,380 VALU per wave = per element), LDS padding to
     // hold 6 (lds 26 KiB) or 5 workgroups per CU like the element kernel
+    {   // two tiles per workgroup (half the grid), loads of the second tile in flight during the first
+        const int ntile = (ne + 255) / 256, half = (ntile + 1) / 2;
+        const int nb2 = (half + 7) / 8 * 8;
+        for (int nv : {0, 1200, 1600}) {
+            const double tv = timeit([&] { hipLaunchKernelGGL(k_prod_2t, dim3(nb2), dim3(256), 0, 0, P, ne, row, nb2 / 8, nv, half); }, 30);
+            printf("{\"num_ele\": %d, \"two_tiles\": 1, \"valu_per_element\": %d, \"ms\": %.4f}\n", ne, nv, tv);
+        }
+    }
     for (int lds : {0, 26 * 1024}) {
         for (int nv : {0, 400, 800, 1200, 1600}) {
             const double tv = timeit([&] { hipLaunchKernelGGL(k_prod_v, dim3(nb), dim3(256), lds, 0, P, ne, row, nb / 8, nv); }, 30);
