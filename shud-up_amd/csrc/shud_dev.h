@@ -65,10 +65,6 @@ enum ClassField {
     CF_ekA, CF_ekB,         // infKsatV * (1 - hAreaF),  hAreaF * macKsatV
     // correctly rounded reciprocals of the class-constant divisors (cdiv, shud_physics.h)
     CF_r_fcmr, CF_r_dTh, CF_r_infD, CF_r_Sy,
-    // roughness-pair table offsets (two int32 in one 8-B slot, byte offsets into the table words): low = this
-    // class's row (table base included), high = its column; the pair {n, RN(1/n)} of an element of class a and a
-    // neighbour of class b sits at low(a) + high(b)
-    CF_rpair,
     CF_COUNT
 };
 // record stride of the class table (8-B words), odd: lanes reading one field of different classes from the
@@ -89,19 +85,10 @@ constexpr int kLdsClassMax = SHUD_LDS_CLS_MAX;
 // most classes a 1024-thread workgroup stages in LDS (600 x 33 x 8 B = 155 KiB of the CU's 160 KiB: one workgroup
 // per CU, 4 waves/SIMD) — models with 129..600 distinct parameter tuples
 constexpr int kLdsClassMaxBig = 600;
-// Manning's n of a lateral edge is avgRough = 0.5 * (Rough_i + Rough_j) (Element.cpp:249-265): a function of the two
-// elements' roughness values, of which a model has a few (land-cover classes).  With <= kRoughPairMax distinct values
-// the class table is followed by the pair table {n, RN(1/n)} [npr][npr] (16-B entries, 16-B aligned), and the
-// kernel divides by n through cdiv; otherwise (npr = 0) it forms n and divides.
-constexpr int kRoughPairMax = 16;
-__host__ __device__ inline int rpair_base_words(int ncls) { return (ncls * (CF_COUNT | 1) + 1) & ~1; }
 
 struct DevPacked {
-    const double *ctab;     // [ncls][CF_STRIDE] record-major: one class's fields share 2-3 cache lines; then the
-                            //   roughness-pair table at word rpair_base_words(ncls) when npr > 0
+    const double *ctab;     // [ncls][CF_STRIDE] record-major: one class's fields share 2-3 cache lines
     int ncls;
-    int npr;                // distinct roughness values in the pair table (0: none)
-    int ntab;               // words of ctab the kernel stages (class table + pair table)
     const double2 *zz;      // {z_surf, z_bottom}  (aquifer_depth == z_surf - z_bottom, checked at create)
     const int4 *meta;       // {nabr0, nabr1, nabr2, cf}: cf bits 0-7 iBC (int8), 8-9 iSS class,
                             //   10-15 #river segments, 16-30 class id, 31 lake element
@@ -135,8 +122,6 @@ struct DevPacked {
 };
 // SHUD_RCP mask the packed element kernel was compiled with (shud_ele_packed.hip)
 int shud_ele_rcp_mask();
-// whether that kernel divides by Manning's n through the roughness-pair table (SHUD_MPAIR)
-int shud_ele_mpair();
 
 struct DevDiag {                     // optional diagnostic outputs (ShudFluxOut), local numbering
     double *qele_surf, *qele_sub, *qele_surf_tot, *qele_sub_tot, *q_infil, *q_exfil, *q_recharge;

@@ -58,11 +58,6 @@ __device__ __forceinline__ T *atw(T *b, uint32_t off) { return (T *)((char *)b +
 #define SHUD_RCP 0
 #endif
 int shud_ele_rcp_mask() { return SHUD_RCP; }
-// SHUD_MPAIR=0: Manning's n formed and divided per edge even when the handle built the roughness-pair table (A/B)
-#ifndef SHUD_MPAIR
-#define SHUD_MPAIR 0
-#endif
-int shud_ele_mpair() { return SHUD_MPAIR; }
 #ifndef SHUD_AREA_EARLY
 #define SHUD_AREA_EARLY 1
 #endif
@@ -137,7 +132,7 @@ __device__ __forceinline__ OwnRec load_own(const DevPacked &p, const YView &Y, i
 constexpr int kTabBatch = 8;
 template <int BS>
 __device__ __forceinline__ void tab_issue(const DevPacked &p, double (&tv)[kTabBatch]) {
-    const int nt = p.ntab;
+    const int nt = p.ncls * CF_LDS_STRIDE;
 #pragma unroll
     for (int k = 0; k < kTabBatch; k++) {
         const int t = (int)threadIdx.x + k * BS;
@@ -146,7 +141,7 @@ __device__ __forceinline__ void tab_issue(const DevPacked &p, double (&tv)[kTabB
 }
 template <int BS>
 __device__ __forceinline__ void tab_store(const DevPacked &p, const double (&tv)[kTabBatch], double *lct) {
-    const int nt = p.ntab;
+    const int nt = p.ncls * CF_LDS_STRIDE;
 #pragma unroll
     for (int k = 0; k < kTabBatch; k++) {
         const int t = (int)threadIdx.x + k * BS;
@@ -158,54 +153,27 @@ __device__ __forceinline__ void tab_store(const DevPacked &p, const double (&tv)
 // passed by the launcher, so no workgroup reads the grid size from the dispatch packet at its start
 __device__ __forceinline__ int tile_of(int per8) { return (int)(blockIdx.x & 7) * per8 + (int)(blockIdx.x >> 3); }
 
-template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, bool GL = false>
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
 __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, const YView &Y, double *__restrict__ dy,
                                          int i, int cur, const DevDiag &dg, const DevLake &lk, const double *lct,
                                          const OwnRec &own);
-
-// SHUD_GED_LDS: the element's three {edge, Dist2Nabor} records (the only HBM stream the edge loop reads) are sent
-// straight into LDS by global_load_lds right after the own record (16 B per lane, no VGPRs held in flight), so an
-// edge iteration waits only for its neighbour gathers, not for an HBM round trip; 3 KiB per wave after the class
-// table.  256-thread kernels with the LDS class table only.
-#ifndef SHUD_GED_LDS
-#define SHUD_GED_LDS 0
-#endif
-#ifndef SHUD_PRIO
-#define SHUD_PRIO 0
-#endif
-typedef __attribute__((address_space(3))) char lds_char;
-constexpr int kGedWave = 3 * 64 * 16;                     // bytes per wave: [edge][lane] double2
-__device__ __forceinline__ size_t ged_lds_off(const DevPacked &p) { return (size_t)((p.ntab + 1) & ~1) * sizeof(double); }
-__device__ __forceinline__ lds_char *ged_wave_lds(const DevPacked &p, double *lct) {
-    return (lds_char *)((char *)lct + ged_lds_off(p)) + (threadIdx.x >> 6) * kGedWave;
-}
-__device__ __forceinline__ void ged_dma(const DevPacked &p, int NEl, int i, lds_char *w) {
-#pragma unroll
-    for (int j = 0; j < 3; j++)
-        __builtin_amdgcn_global_load_lds(p.ged + (size_t)j * NEl + i, (__attribute__((address_space(3))) void *)(w + j * 1024),
-                                         16, 0, 0);
-    __asm__ volatile("" ::: "memory");                    // keep the DMA issue here (the compiler sinks it otherwise)
-}
 
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
 __global__ void __launch_bounds__(256, SHUD_ELE_WAVES)
 shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int i0, int n_compute, int cur,
                        DevDiag dg, DevLake lk, int per8) {
-    extern __shared__ double lct[];                       // p.ntab doubles when LCT
+    extern __shared__ double lct[];                       // ncls * CF_LDS_STRIDE doubles when LCT
     const int i = i0 + tile_of(per8) * 256 + (int)threadIdx.x;   // elements [i0, n_compute)
     const bool act = i < n_compute;
-    if (SHUD_PRIO) __builtin_amdgcn_s_setprio(SHUD_PRIO);     // A/B: a starting wave issues its loads first
     double tv[kTabBatch];
     if (LCT) tab_issue<256>(p, tv);
     OwnRec own;
-    constexpr bool GL = SHUD_GED_LDS && LCT;
     if (act) own = load_own<FU1, GH>(p, Y, i, cur);
-    if (SHUD_PRIO) __builtin_amdgcn_s_setprio(0);
     if (LCT) {
         tab_store<256>(p, tv, lct);
         __syncthreads();
     }
-    if (act) ele_body<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH, GL>(m, p, Y, dy, i, cur, dg, lk, lct, own);
+    if (act) ele_body<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH>(m, p, Y, dy, i, cur, dg, lk, lct, own);
 }
 
 // 129..kLdsClassMaxBig classes: the same body with the class table in LDS, staged by 1024-thread workgroups (one
@@ -266,7 +234,7 @@ shud_ele_kernel_packed_fold(DevMesh m, DevPacked p, YView Y, double *__restrict_
         if (act) own = load_own<FU1, false>(p, Y, i, cur);
         tab_store<256>(p, tv, lct);
         __syncthreads();
-        if (act) ele_body<MODE, OPEN, false, FU1, true, false, false, SHUD_GED_LDS>(m, p, Y, dy, i, cur, dg, lk, lct, own);
+        if (act) ele_body<MODE, OPEN, false, FU1, true, false, false>(m, p, Y, dy, i, cur, dg, lk, lct, own);
         return;
     }
     const int i = n_int + ((int)blockIdx.x - nb_int) * 256 + (int)threadIdx.x;
@@ -278,7 +246,7 @@ shud_ele_kernel_packed_fold(DevMesh m, DevPacked p, YView Y, double *__restrict_
     if (act) own = load_own<FU1, true>(p, Y, i, cur);
     tab_store<256>(p, tv, lct);
     __syncthreads();
-    if (act) ele_body<MODE, OPEN, false, FU1, true, false, true, SHUD_GED_LDS>(m, p, Y, dy, i, cur, dg, lk, lct, own);
+    if (act) ele_body<MODE, OPEN, false, FU1, true, false, true>(m, p, Y, dy, i, cur, dg, lk, lct, own);
 }
 // Producer: the halo's bytes were written by earlier kernels of the comm stream (pack + RCCL, or the test's copy
 // kernel), complete before this one starts; the flag store follows an agent-scope release with an explicit
@@ -302,13 +270,12 @@ __global__ void shud_copy_f64_kernel(double *__restrict__ dst, const double *__r
         dst[k] = src[k];
 }
 
-template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, bool GL>
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
 __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, const YView &Y, double *__restrict__ dy,
                                          int i, int cur, const DevDiag &dg, const DevLake &lk, const double *lct,
                                          const OwnRec &own) {
     const int NEl = m.num_ele;
     const int nown = Y.n_own;
-
     // ---------------- own records (loaded by the caller); saturation (its two pow calls are the register peak) is
     // computed while little else is live ----------------
     const uint32_t o16 = (uint32_t)i << 4, o8 = (uint32_t)i << 3;
@@ -350,10 +317,6 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
             satkr = sat_kfun(satn, CL(ex1), CL(ex2));                    // n/(n-1), (n-1)/n
         }
     }
-
-    // the edge records' DMA, issued once uGW (whose BC-table load would otherwise wait behind it) has been used: it
-    // lands during the rest of the vertical physics
-    if (GL) ged_dma(p, NEl, i, ged_wave_lds(p, (double *)lct));
 
     const int sfl = own.sfl;
     const int sfirst = sfl & 0x7fffffff;
@@ -437,12 +400,6 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
 
     // ---- own river segments (fun_Seg_surface / fun_Seg_sub) and Qe2r (PassValue) ----
     const double dep = CL(depression), rgh = CL(rough);
-    // roughness-pair table (uniform: p.npr): this class's row offset; a neighbour's column offset is added per edge
-#define CLI(f, hi) (LCT ? ((const int *)(lct + cid * CF_LDS_STRIDE + CF_##f))[hi] \
-                        : ((const int *)(p.ctab + cid * CF_STRIDE + CF_##f))[hi])
-    const bool mpair = SHUD_MPAIR == 2 || (SHUD_MPAIR && p.npr > 0);   // 2: ISA counting only
-    const uint32_t prow = mpair ? (uint32_t)CLI(rpair, 0) : 0u;
-#undef CLI
     double qe2r_surf = 0., qe2r_sub = 0.;
     if (nseg) {
         const double isf_seg = rmax(0., usf - q_infil + q_exfil);
@@ -493,12 +450,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
         // (edge 0's loads issued right after the own record instead — held through the vertical physics — took
         // the kernel to 96 VGPRs with spills and measured 0.707 vs 0.617 ms, profiles/r03/ab_prologue/)
         const uint32_t n16 = (uint32_t)nc << 4, n8 = (uint32_t)nc << 3;
-        double2 g;
-        if (GL) {                                         // landed by ged_dma (the compiler waits on its vmcnt)
-            const v2d gv = *(const __attribute__((address_space(3))) v2d *)(ged_wave_lds(p, (double *)lct) + j * 1024 +
-                                                                          16 * (threadIdx.x & 63));
-            g = make_double2(gv.x, gv.y);
-        } else g = ldnt2(at(p.ged + (size_t)j * NEl, o16));
+        const double2 g = ldnt2(at(p.ged + (size_t)j * NEl, o16));
         const double2 nzz = *at(p.zz, n16);
         const int ncf = *at((const int *)p.meta + 3, n16);
         const double nsf_raw = GH ? Y.sf(nc) : *at(Y.y, n8);
@@ -544,13 +496,6 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
                 const double s = D2N_DIV(dh);
                 if (s > 0 && isf <= 0) qsf = 0.;
                 else if (s < 0 && nsf <= 0) qsf = 0.;
-                else if (mpair) {                         // avgRough and RN(1/avgRough) from the pair table
-                    const uint32_t off = prow + (uint32_t)(LCT ? ((const int *)(lct + cn * CF_LDS_STRIDE + CF_rpair))[1]
-                                                               : ((const int *)(p.ctab + cn * CF_STRIDE + CF_rpair))[1]);
-                    const double2 nr = LCT ? *(const double2 *)((const char *)lct + off)
-                                           : *(const double2 *)((const char *)p.ctab + off);
-                    qsf = manning_c(ym * B, nr.x, nr.y, ym, s);
-                }
                 else qsf = manning(ym * B, 0.5 * (rgh + CN(rough)), ym, s);   // avgRough, Element.cpp:253
             }
             const double ugn = ugw_pk<MODE>(m, ngw_raw, cf_ibc(ncf), nb);
@@ -668,10 +613,6 @@ __device__ __forceinline__ double riv_down_outlet(const RivP &q, double uq, cons
 // reaches, bit 1 the segment gathers, bit 2 the downstream reach
 #ifndef SHUD_RIV_ABL
 #define SHUD_RIV_ABL 0
-#endif
-// SHUD_RIV_SEGMASK: segment gathers masked to each reach's own segments (A/B; 0: clamped to the first segment)
-#ifndef SHUD_RIV_SEGMASK
-#define SHUD_RIV_SEGMASK 0
 #endif
 // SHUD_RIV_V: 1 = one chain per neighbour (production), 2 = dependence-ordered loads (A/B)
 #ifndef SHUD_RIV_V
@@ -846,20 +787,11 @@ shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     } else
     for (int k0 = ii.z, k1 = ii.z + ii.w; k0 < k1; k0 += 8) {
         int ps[8];
-        double2 qv[8];
-#if SHUD_RIV_SEGMASK
-        // lanes past their reach's last segment issue no request (a divergent gather costs the address unit one
-        // request per active lane, whatever line it hits)
-#pragma unroll
-        for (int j = 0; j < 8; j++) ps[j] = k0 + j < k1 ? m.rseg_pos[k0 + j] : 0;
-#pragma unroll
-        for (int j = 0; j < 8; j++) qv[j] = k0 + j < k1 ? p.qseg2[ps[j]] : make_double2(0., 0.);
-#else
 #pragma unroll
         for (int j = 0; j < 8; j++) ps[j] = m.rseg_pos[k0 + j < k1 ? k0 + j : k0];
+        double2 qv[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) qv[j] = p.qseg2[ps[j]];
-#endif
 #pragma unroll
         for (int j = 0; j < 8; j++)
             if (k0 + j < k1) { qsurf += qv[j].x; qsub += qv[j].y; }
@@ -1005,13 +937,12 @@ static void launch_big(const DevMesh &m, const DevPacked &p, const YView &Y, dou
                        const DevDiag &dg, const DevLake &lk, hipStream_t s) {
     int nb = (i1 - i0 + 1023) / 1024;
     nb = (nb + 7) / 8 * 8;                  // block_id<1> deals blocks to XCDs in contiguous chunks
-    const size_t lds = (size_t)p.ntab * sizeof(double);
+    const size_t lds = (size_t)p.ncls * CF_LDS_STRIDE * sizeof(double);
     auto *fn = shud_ele_kernel_packed_big<MODE, OPEN, DIAG, FU1, GH>;
     static bool attr = false;               // dynamic LDS above 64 KiB must be allowed per kernel
     if (!attr) {
         (void)hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)((rpair_base_words(kLdsClassMaxBig) + 2 * kRoughPairMax * kRoughPairMax) *
-                                        sizeof(double)));
+                                  (int)(kLdsClassMaxBig * CF_LDS_STRIDE * sizeof(double)));
         attr = true;
     }
     hipLaunchKernelGGL(fn, dim3(nb), dim3(1024), lds, s, m, p, Y, dy, i0, i1, cur, dg, lk, nb / 8);
@@ -1022,7 +953,7 @@ static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, doubl
                      const DevDiag &dg, const DevLake &lk, hipStream_t s) {
     int nb = (i1 - i0 + 255) / 256;
     nb = (nb + 7) / 8 * 8;                  // block_id<1> deals blocks to XCDs in contiguous chunks
-    const size_t lds = LCT ? (size_t)((p.ntab + 1) & ~1) * sizeof(double) + (SHUD_GED_LDS ? 4 * kGedWave : 0) : 0;
+    const size_t lds = LCT ? (size_t)p.ncls * CF_LDS_STRIDE * sizeof(double) : 0;
     hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH>), dim3(nb), dim3(256), lds, s, m, p,
                        Y, dy, i0, i1, cur, dg, lk, nb / 8);
 }
@@ -1066,7 +997,7 @@ bool launch_element_kernel_packed_fold(const DevMesh &m, const DevPacked &p, con
                                        const HaloWait &hw, hipStream_t s) {
     if (n_int <= 0 || n_all <= n_int || p.ncls > LDS_CLS_MAX) return false;
     const int nb_int = ((n_int + 255) / 256 + 7) / 8 * 8, nb_b = (n_all - n_int + 255) / 256;
-    const size_t lds = (size_t)((p.ntab + 1) & ~1) * sizeof(double) + (SHUD_GED_LDS ? 4 * kGedWave : 0);
+    const size_t lds = (size_t)p.ncls * CF_LDS_STRIDE * sizeof(double);
 #define LF(MO, OP, FU) hipLaunchKernelGGL((shud_ele_kernel_packed_fold<MO, OP, FU>), dim3(nb_int + nb_b), dim3(256), lds, \
                                           s, m, p, Y, dy, n_int, n_all, cur, dg, nb_int / 8, nb_int, hw)
     if (mode == 0) {

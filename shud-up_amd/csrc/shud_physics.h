@@ -92,12 +92,6 @@ __device__ __forceinline__ double manning(double A, double n, double R, double S
     const double t = SDIV(SSQRT(pos ? S : -S) * A * pow23(R), n);
     return pos ? t : -t;
 }
-// manning with the divisor's correctly rounded reciprocal (the roughness-pair table): same bits as manning
-__device__ __forceinline__ double manning_c(double A, double n, double rn, double R, double S) {
-    const bool pos = S > 0;
-    const double t = CDIV_(SSQRT(pos ? S : -S) * A * pow23(R), n, rn);
-    return pos ? t : -t;
-}
 // Equations.cpp:116-134 (range check reported by the caller).  The two macropore branches divide different
 // numerators by different divisors; the numerator and divisor are selected per branch and ONE division follows
 // the join, so a wave whose lanes take both branches runs one division sequence instead of two (same operations

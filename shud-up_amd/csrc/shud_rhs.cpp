@@ -413,41 +413,7 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         t[CF_r_dTh] = 1. / t[CF_dTh];
         t[CF_r_infD] = 1. / t[CF_infD];
         t[CF_r_Sy] = 1. / t[CF_Sy];
-        t[CF_rpair] = 0.;
         for (int f = 0; f < CF_COUNT; f++) ctab[(size_t)c * CF_STRIDE + f] = t[f];
-    }
-    // roughness-pair table (shud_dev.h kRoughPairMax): distinct roughness values (by bits) in first-seen class order,
-    // n = 0.5 * (r_a + r_b) as the kernel forms avgRough, RN(1/n) on the host; only when every n is a cdiv divisor
-    int npr = 0;
-    {
-        std::vector<double> rv;
-        std::vector<int> rid(ncls);
-        for (int c = 0; c < ncls && (int)rv.size() <= kRoughPairMax; c++) {
-            const double r = table[c][CF_rough];
-            int k = 0;
-            while (k < (int)rv.size() && memcmp(&rv[k], &r, sizeof(double))) k++;
-            if (k == (int)rv.size()) rv.push_back(r);
-            rid[c] = k;
-        }
-        const int R = (int)rv.size();
-        bool ok = R <= kRoughPairMax && shud_ele_mpair();
-        for (int a = 0; ok && a < R; a++)
-            for (int b = 0; b < R; b++) ok = ok && cdiv_divisor_ok(0.5 * (rv[a] + rv[b]));
-        if (ok) {
-            npr = R;
-            const int base = rpair_base_words(ncls);
-            ctab.resize((size_t)base + 2 * (size_t)R * R, 0.0);
-            for (int a = 0; a < R; a++)
-                for (int b = 0; b < R; b++) {
-                    const double n = 0.5 * (rv[a] + rv[b]);
-                    ctab[(size_t)base + 2 * ((size_t)a * R + b)] = n;
-                    ctab[(size_t)base + 2 * ((size_t)a * R + b) + 1] = 1. / n;
-                }
-            for (int c = 0; c < ncls; c++) {
-                const int32_t off[2] = {(int32_t)(8 * base + 16 * rid[c] * R), (int32_t)(16 * rid[c])};
-                memcpy(&ctab[(size_t)c * CF_STRIDE + CF_rpair], off, sizeof(off));
-            }
-        }
     }
     std::vector<double2> zz(NE), ged(3 * (size_t)NE);
     std::vector<int4> meta(NE);
@@ -473,7 +439,7 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     if ((rc = h->upload(&ged_d, ged.data(), ged.size()))) return rc;
     if ((rc = h->upload(&area_d, m->area, NE))) return rc;
     if ((rc = h->upload(&sf_d, sfirst.data(), NE))) return rc;
-    P.ctab = ctab_d; P.ncls = ncls; P.npr = npr; P.ntab = (int)ctab.size(); P.zz = zz_d; P.meta = meta_d; P.ged = ged_d; P.area = area_d;
+    P.ctab = ctab_d; P.ncls = ncls; P.zz = zz_d; P.meta = meta_d; P.ged = ged_d; P.area = area_d;
     P.seg_first = sf_d;
     // host reciprocals of static geometric divisors for a kernel built with SHUD_RCP (A/B builds)
     const int rcp = shud_ele_rcp_mask();
