@@ -45,6 +45,11 @@ constexpr int NLS_MAXCOR = 3;
 #define SHUD_ODE_LAZY_COMPLETE 1
 #endif
 constexpr bool kLazyComplete = SHUD_ODE_LAZY_COMPLETE != 0;
+// SHUD_ODE_LAZY_ZN0=0: the complete+ewt pass stores zn[0] (only zn[1..q] deferred; A/B)
+#ifndef SHUD_ODE_LAZY_ZN0
+#define SHUD_ODE_LAZY_ZN0 1
+#endif
+constexpr int kLazyZn0 = SHUD_ODE_LAZY_ZN0 != 0;
 constexpr double CVLS_EPLIN = 0.05, CVLS_DGMAX = 0.2;
 constexpr int CVLS_MSBJ = 51;
 enum { FIRST_CALL = 0, PREV_CONV_FAIL = 1, PREV_ERR_FAIL = 2 };
@@ -196,14 +201,19 @@ struct shud_ode {
     // not stored, acor_lazy), which the cvNls start that always follows it would otherwise do in a separate pass
     // (k_vsum_zero)
     bool y_pred = false;
-    // the last step's cvCompleteStep on zn[1..q] (+ zn[qmax] = acor) and a following cvRescale, deferred into the
-    // next pass that reads zn[1..q] (ode::Pend; zn[0] is completed at once by complete_step_ewt)
+    // the last step's cvCompleteStep on zn[0..q] (+ zn[qmax] = acor) and a following cvRescale, deferred into the
+    // next pass that reads zn (ode::Pend; complete_step_ewt forms zn[0]'s new value for the error weights only)
     ode::Pend pend{};
     void materialize() {                                             // apply a deferred completion now
         if (!pend.acor) return;
-        complete_step(n, zn, pend.acor, pend.l, 1, pend.q, pend.copy_to, s);
+        complete_step(n, zn, pend.acor, pend.l, pend.j0, pend.q, pend.copy_to, s);
         if (pend.resc) ode::rescale(n, zn, pend.q, pend.r, s);
         pend = ode::Pend{};
+    }
+    void materialize0() {                                            // zn[0] only (an API read of y(tcur))
+        if (!pend.acor || pend.j0 != 0) return;
+        complete_step(n, zn, pend.acor, pend.l, 0, 0, -1, s);
+        pend.j0 = 1;
     }
     void predict() {
         tn += h;
@@ -575,14 +585,15 @@ struct shud_ode {
         // cvCompleteStep + the next loop iteration's cvEwtSet / N_VWrmsNorm(zn[0]) in one pass (ewt_and_norm);
         // SHUD_ODE_LAZY_COMPLETE: that pass completes zn[0] only, zn[1..q] and the acor copy ride in the next predict
         if (kLazyComplete) {
-            complete_step_ewt(n, zn, acor, lc, 0, -1, rtol, atol, ewt_alt, rs(S_EWTMIN), s);
+            complete_step_ewt(n, zn, acor, lc, 0, -1, kLazyZn0, rtol, atol, ewt_alt, rs(S_EWTMIN), s);
             pend = ode::Pend{};
             pend.acor = acor;
             pend.l = lc;
             pend.q = q;
             pend.copy_to = copy_to;
+            pend.j0 = kLazyZn0 ? 0 : 1;
         } else {
-            complete_step_ewt(n, zn, acor, lc, q, copy_to, rtol, atol, ewt_alt, rs(S_EWTMIN), s);
+            complete_step_ewt(n, zn, acor, lc, q, copy_to, 0, rtol, atol, ewt_alt, rs(S_EWTMIN), s);
         }
         finalize(rs(S_EWTMIN), 2, 1u, s);
         ewt_pending = true;
@@ -691,12 +702,17 @@ struct shud_ode {
             if (n_sync == ewt_fin_sync && !fetch()) return -1;          // no synchronize since its finalize
             return h_ds[S_EWTMIN] <= 0.0 ? 1 : 0;
         }
+        materialize0();
         ewt_set(n, Z(0), ewt, rtol, atol, rs(S_EWTMIN), s);
         finalize(rs(S_EWTMIN), 2, 1u, s);
         if (!fetch()) return -1;
         return h_ds[S_EWTMIN] <= 0.0 ? 1 : 0;
     }
-    void out_y(double *yout) { if (yout) copy(n, Z(0), yout, s); }
+    void out_y(double *yout) {
+        if (!yout) return;
+        materialize0();
+        copy(n, Z(0), yout, s);
+    }
 
     int solve(double tout, double *yout, double *tret, int itask) {   // CVode
         int istate = SHUD_ODE_SUCCESS;
@@ -945,7 +961,11 @@ extern "C" int shud_ode_get_stats(shud_ode_t o, ShudOdeStats *st) {
     return SHUD_ODE_SUCCESS;
 }
 
-extern "C" const double *shud_ode_state_device(shud_ode_t o) { return o ? o->zn : nullptr; }
+extern "C" const double *shud_ode_state_device(shud_ode_t o) {
+    if (!o) return nullptr;
+    o->materialize0();                 // zn[0]'s completion may still be pending (ode::Pend)
+    return o->zn;
+}
 
 extern "C" int shud_ode_destroy(shud_ode_t o) {
     if (!o) return SHUD_ODE_MEM_NULL;

@@ -56,14 +56,15 @@ struct Coefs {         // small host-computed coefficient arrays passed by value
     double c[kMaxL + 1];
 };
 
-// A deferred cvCompleteStep on zn[1..q] (zn[j] = l[j]*acor + zn[j]) and its zn[copy_to] = acor, and a deferred
-// cvRescale after it (zn[j] *= r[j], j = 1..q): applied in registers by the first pass that reads zn[1..q] (the
-// next cvPredict, a CVodeGetDky, cvComputeEtaqm1's norm), or materialized before an order change.  zn[0] is always
-// completed at once (the ewt pass needs it).  acor == nullptr: nothing pending.
+// A deferred cvCompleteStep on zn[j0..q] (zn[j] = l[j]*acor + zn[j]) and its zn[copy_to] = acor, and a deferred
+// cvRescale after it (zn[j] *= r[j], j = 1..q): applied in registers by the first pass that reads zn (the next
+// cvPredict, a CVodeGetDky, cvComputeEtaqm1's norm), or materialized before an order change / a read of zn[0]
+// through the API.  j0 = 0: zn[0] pending too (the ewt pass computes it without storing it).  acor == nullptr:
+// nothing pending.
 struct Pend {
     const double *acor;
     Coefs l, r;
-    int q, copy_to, resc;
+    int q, copy_to, resc, j0;
 };
 
 // ---- launchers (hipStream_t s); a reduction kernel leaves per-block partials, finalize(r, nacc, minmask) writes
@@ -110,9 +111,10 @@ int lazy_ycor();
 // zn[j] = l[j]*acor + zn[j], j = jlo..q; if copy_to >= 0: zn[copy_to] = acor
 void complete_step(int64_t n, double *zn, const double *acor, const Coefs &l, int jlo, int q, int copy_to,
                    hipStream_t s);
-// complete_step, then ewt_set's arithmetic on the new zn[0] into ewt_next; r: [min(rtol|y| + atol), sum (y*w)^2]
-void complete_step_ewt(int64_t n, double *zn, const double *acor, const Coefs &l, int q, int copy_to, double rtol,
-                       double atol, double *ewt_next, const Red &r, hipStream_t s);
+// complete_step (columns jst..q stored; zn[0]'s value is formed either way), then ewt_set's arithmetic on the new
+// zn[0] into ewt_next; r: [min(rtol|y| + atol), sum (y*w)^2]
+void complete_step_ewt(int64_t n, double *zn, const double *acor, const Coefs &l, int q, int copy_to, int jst,
+                       double rtol, double atol, double *ewt_next, const Red &r, hipStream_t s);
 // r: [sum (zn_q*ewt)^2 (zn_q != NULL), sum (((-cquot)*zn_qmax + acor)*ewt)^2 (zn_qmax != NULL)]; pend_q: zn_q's
 // completion is pending, zn_q = lq*acor + zn_q on the fly
 void eta_norms(int64_t n, const double *zn_q, const double *zn_qmax, const double *acor, double ncquot,

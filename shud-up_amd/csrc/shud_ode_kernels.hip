@@ -201,6 +201,7 @@ __global__ void __launch_bounds__(kThreads) k_pascal(int64_t n, double *__restri
         return a;
     }, [&](int64_t i, T a) {
         if (PEND) {
+            if (pd.j0 == 0) a.v[0] = pd.l.c[0] * a.v[Q + 1] + a.v[0];
 #pragma unroll
             for (int j = 1; j <= Q; ++j) a.v[j] = pd.l.c[j] * a.v[Q + 1] + a.v[j];
             if (pd.resc) {
@@ -541,7 +542,7 @@ void complete_step(int64_t n, double *zn, const double *acor, const Coefs &l, in
 template <int U>
 __global__ void __launch_bounds__(kRedThreads) k_complete_ewt(int64_t n, double *__restrict__ zn,
                                                               const double *__restrict__ acor, Coefs l, int q,
-                                                              int copy_to, double rtol, double atol,
+                                                              int copy_to, int jst, double rtol, double atol,
                                                               double *__restrict__ ewt_next, Red r) {
     double v[2] = {INFINITY, 0.0};
     using T = DN<kQMax + 2>;
@@ -558,7 +559,7 @@ __global__ void __launch_bounds__(kRedThreads) k_complete_ewt(int64_t n, double 
         for (int j = 0; j <= kQMax; ++j)
             if (j <= q) {
                 const double z = l.c[j] * a.v[0] + a.v[1 + j];
-                stn(zn + (int64_t)j * n + i, z);
+                if (j >= jst) stn(zn + (int64_t)j * n + i, z);      // jst = 1: zn[0]'s completion stays pending
                 if (j == 0) z0 = z;
             }
         if (copy_to >= 0) stn(zn + (int64_t)copy_to * n + i, a.v[0]);
@@ -571,9 +572,9 @@ __global__ void __launch_bounds__(kRedThreads) k_complete_ewt(int64_t n, double 
     });
     block_partial<2>(v, 1u, r);
 }
-void complete_step_ewt(int64_t n, double *zn, const double *acor, const Coefs &l, int q, int copy_to, double rtol,
-                       double atol, double *ewt_next, const Red &r, hipStream_t s) {
-    LAUNCH_RED(k_complete_ewt, r, s, n, zn, acor, l, q, copy_to, rtol, atol, ewt_next);
+void complete_step_ewt(int64_t n, double *zn, const double *acor, const Coefs &l, int q, int copy_to, int jst,
+                       double rtol, double atol, double *ewt_next, const Red &r, hipStream_t s) {
+    LAUNCH_RED(k_complete_ewt, r, s, n, zn, acor, l, q, copy_to, jst, rtol, atol, ewt_next);
 }
 
 // cvComputeEtaqm1 / cvComputeEtaqp1 norms in one pass
@@ -631,7 +632,7 @@ __global__ void __launch_bounds__(kThreads) k_dky(int64_t n, const double *__res
         const double ac = pd.acor ? pd.acor[i] : 0.0;
         auto Zj = [&](int j) {            // zn[j] as completed (k_complete's value when its completion is pending)
             const double z = zn[j * stride + i];
-            return (pd.acor && j >= 1 && j <= pd.q) ? pd.l.c[j] * ac + z : z;
+            return (pd.acor && j >= pd.j0 && j <= pd.q) ? pd.l.c[j] * ac + z : z;
         };
         double z;
         if (nvec == 1) {
