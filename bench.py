@@ -220,8 +220,9 @@ def main():
     torch.cuda.synchronize()
     # HIP events around the kernels of every 2nd timed eval (handle's stream = torch's current stream): an event
     # between two kernels stops their tails overlapping (~1 % of an eval), so only a sample of the K evals
-    # carries them
-    t_stride = 2 if args.steps >= 10 else 1
+    # carries them.  A partitioned rank's eval is ~0.09 ms, where three event records cost ~15 % of the eval
+    # (tools/rank_timing.py: 0.105 ms with events on every eval vs 0.089 without), so N > 1 samples 1 in 4
+    t_stride = (4 if (world > 1 or args.partition_1) else 2) if args.steps >= 10 else 1
     h.timing(args.steps, t_stride)
     if world > 1:
         dist.barrier()
