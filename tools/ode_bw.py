@@ -22,7 +22,8 @@ PER_ENTRY = {
     "k_normalize": lambda q: 24,
     "k_newton_update": lambda q: 8 * (3 + 2),   # ewt, ycor, ~2 Krylov vectors, ycor
     "k_complete": lambda q: 8 * (1 + 2 * q),                # round 4: materializes zn[1..q] (eager: 1 + 2(q+1))
-    "k_complete_ewt": lambda q: 32,         # round 4: acor, zn[0] -> zn[0], ewt (eager: 8 * (1 + 2(q+1)) + 8)
+    "k_complete_ewt": lambda q: 24,         # round 4: acor, zn[0] -> ewt (zn[0] deferred too; --eager-zn0: 32;
+                                            # eager complete: 8 * (1 + 2(q+1)) + 8)
     "k_rescale": lambda q: 16 * q,
     "k_eta_norms": lambda q: 32,
 }
@@ -36,6 +37,7 @@ def main():
     ap.add_argument("--eager-ycor", action="store_true", help="sources before the lazy ycor (predict stores ycor = 0)")
     ap.add_argument("--eager-complete", action="store_true",
                     help="sources before round 4's deferred cvCompleteStep (complete_ewt updates all of zn)")
+    ap.add_argument("--eager-zn0", action="store_true", help="sources where complete_ewt still stores zn[0]")
     ap.add_argument("--copy-gbs", type=float, default=6400.0, help="the box's STREAM copy rate")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.csv)))
@@ -59,6 +61,8 @@ def main():
             b = PER_ENTRY[key](a.q)
             if a.eager_complete and key == "k_complete":
                 b = 8 * (1 + 2 * (a.q + 1))
+            if a.eager_zn0 and key == "k_complete_ewt":
+                b = 32
             if a.eager_complete and key == "k_complete_ewt":
                 b = 8 * (1 + 2 * (a.q + 1)) + 8
         elif "k_finalize" in name:
