@@ -101,6 +101,8 @@ struct DevPacked {
     const double2 *sg_dk;   //   its reach's {depth, KsatH}
     const int2 *sg_rb;      //   {reach, reach BC column}
     const double *sg_bt;    //   its reach's BedThick
+    const int *sg_r;        // SHUD_SEG_RREC layout: [NS] the segment's (local) reach; with rrec [2 * local reaches]
+    const double2 *rrec;    //   {depth, KsatH}, {BedThick, (BC column, 0) bits} per reach
     double2 *qseg2;         // [NS] {QsegSurf, QsegSub}, written by the element kernel (element-sorted, or
                             //   reach-sorted when seg_rpos is set)
     const int *seg_rpos;    // nullptr, or element-sorted k -> reach-sorted slot (SHUD_RHS_SEG_ORDER=reach)
@@ -122,6 +124,8 @@ struct DevPacked {
 };
 // SHUD_RCP mask the packed element kernel was compiled with (shud_ele_packed.hip)
 int shud_ele_rcp_mask();
+// whether it reads the per-reach segment records (SHUD_SEG_RREC)
+int shud_ele_seg_rrec();
 
 struct DevDiag {                     // optional diagnostic outputs (ShudFluxOut), local numbering
     double *qele_surf, *qele_sub, *qele_surf_tot, *qele_sub_tot, *q_infil, *q_exfil, *q_recharge;

@@ -58,6 +58,13 @@ __device__ __forceinline__ T *atw(T *b, uint32_t off) { return (T *)((char *)b +
 #define SHUD_RCP 0
 #endif
 int shud_ele_rcp_mask() { return SHUD_RCP; }
+// SHUD_SEG_RREC (default): segments stream {length, Cwr} + a reach index and gather their reach's statics from one
+// 32-B per-reach record (−28 B of HBM per segment); 0: a 48-B segment record with the reach's statics copied into
+// it (A/B, rounds 1-3)
+#ifndef SHUD_SEG_RREC
+#define SHUD_SEG_RREC 1
+#endif
+int shud_ele_seg_rrec() { return SHUD_SEG_RREC; }
 #ifndef SHUD_AREA_EARLY
 #define SHUD_AREA_EARLY 1
 #endif
@@ -405,10 +412,21 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
         const double isf_seg = rmax(0., usf - q_infil + q_exfil);
         for (int k = sfirst, k1 = k + nseg; k < k1; k++) {
             // one 48-B element-sorted record per segment: its own fields plus its reach's statics
-            const uint32_t k16 = (uint32_t)k << 4, k8 = (uint32_t)k << 3;
+            const uint32_t k16 = (uint32_t)k << 4;
+            [[maybe_unused]] const uint32_t k8 = (uint32_t)k << 3;
+#if SHUD_SEG_RREC
+            // 20 B per segment streamed ({length, Cwr} + its reach); the reach's {depth, KsatH | BedThick, BC} is one
+            // 32-B record shared by the reach's ~5 segments (a gather beside the stage gather, mostly cache hits)
+            const double2 lc = *at(p.sg_lc, k16);
+            const int rr = *at(p.sg_r, (uint32_t)k << 2);
+            const double2 dk = p.rrec[2 * (size_t)rr], rx = p.rrec[2 * (size_t)rr + 1];
+            const int2 rb = make_int2(rr, __builtin_bit_cast(int2, rx.y).x);
+            const double bt = rx.x;
+#else
             const double2 lc = *at(p.sg_lc, k16), dk = *at(p.sg_dk, k16);
             const int2 rb = *at(p.sg_rb, k8);
             const double bt = *at(p.sg_bt, k8);
+#endif
             // (the first segment's reach index + stage loaded at the top of the body instead, in flight across the
             // vertical physics: 88 VGPRs, 0.625 vs 0.623 ms — not kept, profiles/r03/ab_river2/)
             double yr = GH ? Y.riv(rb.x) : *at(Y.y + 3 * (size_t)nown, (uint32_t)rb.x << 3);   // uriv_of, BC below

@@ -478,10 +478,29 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         }
         double2 *lc_d, *dk_d; int2 *rb_d; double *bt_d;
         if ((rc = h->upload(&lc_d, lc.data(), NSg))) return rc;
-        if ((rc = h->upload(&dk_d, dk.data(), NSg))) return rc;
-        if ((rc = h->upload(&rb_d, rb.data(), NSg))) return rc;
-        if ((rc = h->upload(&bt_d, bt.data(), NSg))) return rc;
-        P.sg_lc = lc_d; P.sg_dk = dk_d; P.sg_rb = rb_d; P.sg_bt = bt_d;
+        P.sg_lc = lc_d;
+        if (shud_ele_seg_rrec()) {                     // segments -> per-reach records (shud_dev.h sg_r / rrec)
+            const int NRl = m->num_riv;
+            std::vector<int> sr(NSg);
+            std::vector<double2> rr(2 * (size_t)NRl);
+            for (int k = 0; k < NSg; k++) sr[k] = rb[k].x;
+            for (int r = 0; r < NRl; r++) {
+                const int32_t two[2] = {m->riv_bc ? m->riv_bc[r] : 0, 0};
+                double bits;
+                memcpy(&bits, two, sizeof bits);
+                rr[2 * (size_t)r] = make_double2(m->riv_depth[r], m->riv_ksath[r]);
+                rr[2 * (size_t)r + 1] = make_double2(m->riv_bedthick[r], bits);
+            }
+            int *sr_d; double2 *rr_d;
+            if ((rc = h->upload(&sr_d, sr.data(), NSg))) return rc;
+            if ((rc = h->upload(&rr_d, rr.data(), rr.size()))) return rc;
+            P.sg_r = sr_d; P.rrec = rr_d;
+        } else {
+            if ((rc = h->upload(&dk_d, dk.data(), NSg))) return rc;
+            if ((rc = h->upload(&rb_d, rb.data(), NSg))) return rc;
+            if ((rc = h->upload(&bt_d, bt.data(), NSg))) return rc;
+            P.sg_dk = dk_d; P.sg_rb = rb_d; P.sg_bt = bt_d;
+        }
         if (rcp & 4) {
             std::vector<double> rbt(NSg);
             for (int k = 0; k < NSg; k++) {
