@@ -35,9 +35,11 @@ def per_kernel(d, counter):
 
 # single-use coalesced read streams, bytes per element / reach / segment (the packed layout, shud_dev.h):
 # element kernel: meta 16, zz 16, y 24, {net_prep, pot_evap} 16, {pot_tran, ETP} 16, carried {u_satn, e_ic} 16,
-# seg_first 4, the three edges' {edge, Dist2Nabor} 48, area 8 per element; segment records 48 per segment.
+# seg_first 4, the three edges' {edge, Dist2Nabor} 48, area 8 per element; per segment {length, Cwr} 16 + its
+# reach index 4 (round 4: the reach's statics are a gathered per-reach record, counted with the scattered part;
+# rounds 1-3 streamed a 48-B segment record)
 # river kernel: its 64-B record, rv_i 16, rv_u 16, stage 8 per reach; segment positions 4 per segment.
-COALESCED = {"shud_ele_kernel": (164, 0, 48), "shud_riv_kernel": (0, 104, 4)}
+COALESCED = {"shud_ele_kernel": (164, 0, 20), "shud_riv_kernel": (0, 104, 4)}
 
 
 def main():
