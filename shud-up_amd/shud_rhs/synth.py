@@ -48,7 +48,45 @@ def grid_dims(n_target):
     return nqx, nqy
 
 
-def synth_model(n_target, seed=12345, h=100.0, stem_every=12, reach_quads=3):
+def _down_key(kind, key, rid, reach_quads):
+    """the downstream reach's (kind, key) of a reach, or None at an outlet (synth_model's network rule)"""
+    if kind == "stem":
+        k, j0 = key
+        return ("stem", (k, j0 - reach_quads)) if j0 - reach_quads >= 0 else None
+    k, jr, side, q = key
+    nxt = ("trib", (k, jr, side, q + reach_quads))
+    return nxt if nxt in rid else ("stem", (k, (jr // reach_quads) * reach_quads))
+
+
+def _tree_reach_order(reaches, reach_quads, depth_first=False):
+    """The reaches renumbered from the outlets, breadth-first (each reach's upstream reaches, in their generated
+    order, numbered consecutively and next to the upstream reaches of the reach numbered before it) or
+    depth-first pre-order (a reach's first upstream reach numbered right after it).  A caller
+    numbering for the river-order measurement: same network, same cells, other reach ids."""
+    rid = {(kind, key): n for n, (kind, key, _, _) in enumerate(reaches)}
+    ups = [[] for _ in reaches]
+    outlets = []
+    for n, (kind, key, _, _) in enumerate(reaches):
+        dk = _down_key(kind, key, rid, reach_quads)
+        (outlets if dk is None else ups[rid[dk]]).append(n)
+    if not depth_first:
+        order, head = list(outlets), 0
+        while head < len(order):
+            order.extend(ups[order[head]])
+            head += 1
+    else:   # pre-order: a reach, then each upstream subtree in turn (a chain of single reaches stays contiguous)
+        order, stack = [], list(reversed(outlets))
+        while stack:
+            n = stack.pop()
+            order.append(n)
+            stack.extend(reversed(ups[n]))
+    assert len(order) == len(reaches)
+    return [reaches[n] for n in order]
+
+
+def synth_model(n_target, seed=12345, h=100.0, stem_every=12, reach_quads=3, reach_order="band"):
+    """reach_order: "band" (the generated order: row bands south to north, stems then tributaries) or "bfs"
+    / "dfs" (_tree_reach_order; the segment lengths' random draws then land on other segments)."""
     rng = np.random.default_rng(seed)
     soil, geol, lc, rtype, att_rows, cal = load_tables()
     nqx, nqy = grid_dims(n_target)
@@ -109,6 +147,8 @@ def synth_model(n_target, seed=12345, h=100.0, stem_every=12, reach_quads=3):
                             part = cols[q:q + reach_quads]
                             reaches.append(("trib", (k, jr, side, q), [(ci, jr) for ci in part], 1 + (q // reach_quads) % 3))
     NR = len(reaches)
+    if reach_order in ("bfs", "dfs"):
+        reaches = _tree_reach_order(reaches, reach_quads, depth_first=reach_order == "dfs")
     rid = {(kind, key): n for n, (kind, key, _, _) in enumerate(reaches)}
     down = np.empty(NR, dtype=np.int64)
     rtyp = np.empty(NR, dtype=np.int64)
