@@ -115,8 +115,10 @@ struct DevPacked {
     // depth, (down, BC)}: everything a reach's own, its downstream's and its upstream reaches' QrivDown read,
     // so a neighbour reach costs one cache line instead of one line per field pair
     const double2 *rv;      // [4 * NR]
-    const int4 *rv_i;       // {down, BC, first reach-sorted segment, #segments}
-    const int4 *rv_u;       // {up0, up1, up2, #up} (ascending global order); #up = -1: use up_off/up_idx
+    // one 16-B index word per reach {first reach-sorted segment, #segments | code << 16, w2, w3}: code 0..2 =
+    // that many upstream reaches, in w2, w3; code 3 = more, up_idx[w2 .. w2 + w3) (ascending global order)
+    const int4 *rv_u;
+    int riv_sb;             // segments per batch in the river kernel (6 or 8; choose_riv_sb)
     int lds_big;            // 1: 129..kLdsClassMaxBig classes take the 1024-thread LDS-table kernel (host dispatch)
     // correctly rounded reciprocals of static geometric divisors, uploaded only for a kernel built with the
     // matching SHUD_RCP bit (shud_ele_rcp_mask()): 1 area, 2 Dist2Nabor [3][NE], 4 segment reach BedThick

@@ -632,120 +632,17 @@ __device__ __forceinline__ double riv_down_outlet(const RivP &q, double uq, cons
 #ifndef SHUD_RIV_ABL
 #define SHUD_RIV_ABL 0
 #endif
-// SHUD_RIV_V: 1 = one chain per neighbour (production), 2 = dependence-ordered loads (A/B)
-#ifndef SHUD_RIV_V
-#define SHUD_RIV_V 1
-#endif
-// f_update's clamp (MODE 1) and the BC override on an already loaded stage; *yg = what updateRiver() saw
-template <int MODE>
-__device__ __forceinline__ double riv_stage_v(double yr, int bc, double ybc, double *yg) {
-    if (MODE == 1) yr = (yr >= 0.) ? yr : 0.;
-    *yg = yr;
-    return bc > 0 ? ybc : yr;
-}
-#if SHUD_RIV_V == 2
-constexpr int kRivSegBatch = 8;
-// A reach's operands form a three-level dependence chain: its own record and index words; then its downstream
-// and up to 3 upstream reaches' records and stages and its segments' flux positions; then the segment fluxes.
-// Every load of a level is issued before any of the level's values is used (lanes without an upstream reach
-// masked off: a clamped always-on record load costs the scattered-access path as much as a real one), so a
-// reach costs three memory round trips instead of one per upstream reach and per branch (round 2: ~7 in series).
-// The physics and every sum's order are unchanged.
-template <int MODE, bool DIAG, int ABL = 0>
-__global__ void __launch_bounds__(256)
-shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, DevDiag dg, int per8) {
-    // XCD-chunked workgroup order: a reach's up/downstream records sit a few blocks away in index space,
-    // so they are L2 hits on the same XCD instead of fabric round trips (speed only)
-    const int r = tile_of(per8) * 256 + (int)threadIdx.x;
-    if (r >= Y.n_own_riv) return;
-    // ---- level 1 ----
-    const RivP q = riv_load(p, r);
-    const int4 ii = p.rv_i[r];                                  // {down, BC, first segment, #segments}
-    const int4 up = p.rv_u[r];                                  // {up0, up1, up2, #upstream or -1: CSR}
-    const double yr0 = Y.y[3 * (size_t)Y.n_own + r];
-    // ---- level 2 ----
-    const int d = (!(ABL & 4) && q.down >= 0) ? q.down : r;
-    const int nup = (ABL & 1) ? 0 : up.w;
-    const double2 bd = p.rv[4 * (size_t)d + 1], dd = p.rv[4 * (size_t)d + 3];   // same line of d's record
-    const double yd0 = *riv_y_at(Y, d);
-    RivP qu0, qu1, qu2;
-    double yu0 = 0., yu1 = 0., yu2 = 0.;
-    if (nup > 0) { qu0 = riv_load(p, up.x); yu0 = *riv_y_at(Y, up.x); }
-    if (nup > 1) { qu1 = riv_load(p, up.y); yu1 = *riv_y_at(Y, up.y); }
-    if (nup > 2) { qu2 = riv_load(p, up.z); yu2 = *riv_y_at(Y, up.z); }
-    const double ybc = m.rybc[q.bc > 0 ? q.bc : 0];             // tables hold >= 1 entry
-    const double qbc0 = m.rqbc[q.bc < 0 ? -q.bc : 0];
-    const int ns = (ABL & 2) ? 0 : ii.w;
-    const bool rsort = p.seg_rpos != nullptr;                   // reach-sorted fluxes: contiguous from ii.z
-    int ps[kRivSegBatch];
-#pragma unroll
-    for (int j = 0; j < kRivSegBatch; j++) {   // past the reach's last segment: its first again (same line)
-        const int k = ns > 0 ? ii.z + (j < ns ? j : 0) : 0;
-        ps[j] = rsort ? k : m.rseg_pos[k];
-    }
-    // ---- level 3 ----
-    double2 qv[kRivSegBatch];
-#pragma unroll
-    for (int j = 0; j < kRivSegBatch; j++) qv[j] = p.qseg2[ns > 0 ? ps[j] : 0];
+// dword-aligned 16-B / 8-B loads of index words (gfx950 global loads need only 4-B alignment for dwordx4)
+struct __attribute__((packed, aligned(4))) Int4u { int x, y, z, w; };
+struct __attribute__((packed, aligned(4))) Int2u { int x, y; };
 
-    double yg;
-    const double ur = riv_stage_v<MODE>(yr0, q.bc, ybc, &yg);
-    const RivGeom g = riv_geom_p(q, yg);
-    double qdown = 0.;
-    if (!(ABL & 4)) {
-        const int bcd = rv_ib(dd.y).y;
-        const double ydb = bcd > 0 ? m.rybc[bcd] : 0.;
-        double ydg;
-        const double ud = riv_stage_v<MODE>(yd0, bcd, ydb, &ydg);
-        qdown = riv_down_p(q, ur, g, ud, dd.x, bd.y);
-    }
-    // junction: QrivUp[down] += -QrivDown[i], i ascending (MD_f.cpp:236-240)
-    auto up_term = [&](const RivP &qu, double yu0v) {
-        const double ybu = qu.bc > 0 ? m.rybc[qu.bc] : 0.;
-        double yu;
-        const double uu = riv_stage_v<MODE>(yu0v, qu.bc, ybu, &yu);
-        return -riv_down_p(qu, uu, riv_geom_p(qu, yu), ur, q.depth, q.slope);
-    };
-    double qup = 0.;
-    if (nup > 0) qup += up_term(qu0, yu0);
-    if (nup > 1) qup += up_term(qu1, yu1);
-    if (nup > 2) qup += up_term(qu2, yu2);
-    if (nup < 0)
-        for (int k = m.up_off[r], k1 = m.up_off[r + 1]; k < k1; k++) {
-            const int u = m.up_idx[k];
-            qup += up_term(riv_load(p, u), *riv_y_at(Y, u));
-        }
-    // segment sums, ascending reference segment order (MD_f.cpp:228-235)
-    double qsurf = 0., qsub = 0.;
-#pragma unroll
-    for (int j = 0; j < kRivSegBatch; j++)
-        if (j < ns) { qsurf += qv[j].x; qsub += qv[j].y; }
-    for (int k0 = ii.z + kRivSegBatch, k1 = ii.z + ns; k0 < k1; k0 += kRivSegBatch) {   // > 8 segments
-        int pk[kRivSegBatch];
-#pragma unroll
-        for (int j = 0; j < kRivSegBatch; j++) pk[j] = rsort ? k0 + j : m.rseg_pos[k0 + j < k1 ? k0 + j : k0];
-        double2 qk[kRivSegBatch];
-#pragma unroll
-        for (int j = 0; j < kRivSegBatch; j++) qk[j] = p.qseg2[k0 + j < k1 ? pk[j] : pk[0]];
-#pragma unroll
-        for (int j = 0; j < kRivSegBatch; j++)
-            if (k0 + j < k1) { qsurf += qk[j].x; qsub += qk[j].y; }
-    }
-    const double qbc = q.bc < 0 ? qbc0 : 0.0;
-    double dv;
-    if (q.bc > 0) dv = 0.;
-    else if (MODE == 0) {   // MD_f.cpp:162-166
-        dv = (-qup - qsurf - qsub - qdown + qbc) / q.len;
-        if (dv < -1. * g.csarea) dv = -1. * g.csarea;
-        dv = da_to_dy(dv, g.topw, q.bs);                              // fun_dAtodY functions.hpp:125-153
-    } else {                // MD_f_omp.cpp:59
-        dv = (-qup - qsurf - qsub - qdown + qbc) / g.toparea;
-    }
-    dy[3 * Y.n_own + r] = dv;
-    if (DIAG) { dg.qriv_down[r] = qdown; dg.qriv_up[r] = qup; dg.qriv_surf[r] = qsurf; dg.qriv_sub[r] = qsub; }
-}
-#else
-template <int MODE, bool DIAG, int ABL = 0>
+// The kernel is bound by its load-instruction count per wave, not by bytes (227 MB per launch is 1.07x its unique
+// footprint) nor by neighbour locality (profiles/r04/ab_riv/riv_order*.log): round 4 cut the per-reach loads —
+// one 16-B index word per reach (rv_u, shud_dev.h) instead of two; a many-upstream reach's up_idx slots loaded
+// together from the offset in that word (no up_off load, no index load per upstream reach); a segment batch's
+// flux positions as 16-B (+ 8-B) loads instead of one 4-B load each; SB segments per batch, chosen by the host
+// from the reaches' segment counts (choose_riv_sb, shud_rhs.cpp).  0.0709 -> 0.0605 ms at syn-10M, same bits.
+template <int MODE, bool DIAG, int SB, int ABL = 0>
 __global__ void __launch_bounds__(256)
 shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, DevDiag dg, int per8) {
     // XCD-chunked workgroup order: a reach's up/downstream records sit a few blocks away in index space,
@@ -753,8 +650,8 @@ shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     const int r = tile_of(per8) * 256 + (int)threadIdx.x;
     if (r >= Y.n_own_riv) return;
     const RivP q = riv_load(p, r);
-    const int4 ii = p.rv_i[r];                                  // {down, BC, first segment, #segments}
-    const int4 up = p.rv_u[r];
+    const int4 ru = p.rv_u[r];                  // {first segment, #segments | code << 16, w2, w3}
+    const int seg0 = ru.x, nseg = ru.y & 0xffff, upc = ru.y >> 16;
     double yg;
     const double ur = riv_stage_p<MODE>(m, Y, r, q.bc, &yg);
     const RivGeom g = riv_geom_p(q, yg);
@@ -768,50 +665,58 @@ shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         qdown = riv_down_p(q, ur, g, ud, dd.x, bd.y);
     }
     // junction: QrivUp[down] += -QrivDown[i], i ascending (MD_f.cpp:236-240)
+    auto up_term = [&](int u) {
+        const RivP qu = riv_load(p, u);
+        double yu;
+        const double uu = riv_stage_p<MODE>(m, Y, u, qu.bc, &yu);
+        return -riv_down_p(qu, uu, riv_geom_p(qu, yu), ur, q.depth, q.slope);
+    };
     double qup = 0.;
-    const int nup = (ABL & 1) ? 0 : up.w;
-    if (nup >= 0) {
-        const int uv[3] = {up.x, up.y, up.z};
+    if (ABL & 1) {
+    } else if (upc < 3) {                                       // 0..2 upstream reaches in w2, w3
+        if (upc > 0) qup += up_term(ru.z);
+        if (upc > 1) qup += up_term(ru.w);
+    } else {                                                    // more: up_idx[w2 .. w2 + w3), 8 indices at a time
+        for (int k0 = ru.z, k1 = ru.z + ru.w; k0 < k1; k0 += 8) {
+            int uv[8];
 #pragma unroll
-        for (int k = 0; k < 3; k++) {
-            if (k < nup) {
-                const int u = uv[k];
-                const RivP qu = riv_load(p, u);
-                double yu;
-                const double uu = riv_stage_p<MODE>(m, Y, u, qu.bc, &yu);
-                qup += -riv_down_p(qu, uu, riv_geom_p(qu, yu), ur, q.depth, q.slope);
-            }
-        }
-    } else {
-        for (int k = m.up_off[r], k1 = m.up_off[r + 1]; k < k1; k++) {
-            const int u = m.up_idx[k];
-            const RivP qu = riv_load(p, u);
-            double yu;
-            const double uu = riv_stage_p<MODE>(m, Y, u, qu.bc, &yu);
-            qup += -riv_down_p(qu, uu, riv_geom_p(qu, yu), ur, q.depth, q.slope);
+            for (int j = 0; j < 8; j++) uv[j] = m.up_idx[k0 + j < k1 ? k0 + j : k0];
+#pragma unroll
+            for (int j = 0; j < 8; j++)
+                if (k0 + j < k1) qup += up_term(uv[j]);
         }
     }
     // segment sums, ascending reference segment order (MD_f.cpp:228-235), gathered from the element-sorted
-    // fluxes (scattered 8-B writes from the element kernel cost more than these gathers).  Batches of 8:
-    // all index loads, then all gathers, are in flight together; the adds stay in segment order
+    // fluxes (scattered 8-B writes from the element kernel cost more than these gathers).  Batches of SB:
+    // the positions (16-B loads; rseg_pos is padded by 8 words), then all gathers, are in flight together;
+    // positions past the reach's last segment are replaced by its first (the same line); the adds stay in order
     double qsurf = 0., qsub = 0.;
     if (ABL & 2) {
     } else if (p.seg_rpos) {                            // reach-sorted fluxes: this reach's segments are contiguous
-        for (int k = ii.z, k1 = ii.z + ii.w; k < k1; k++) {
+        for (int k = seg0, k1 = seg0 + nseg; k < k1; k++) {
             const double2 q2 = p.qseg2[k];
             qsurf += q2.x;
             qsub += q2.y;
         }
     } else
-    for (int k0 = ii.z, k1 = ii.z + ii.w; k0 < k1; k0 += 8) {
-        int ps[8];
+    for (int k0 = seg0, k1 = seg0 + nseg; k0 < k1; k0 += SB) {
+        int raw[SB], ps[SB];
 #pragma unroll
-        for (int j = 0; j < 8; j++) ps[j] = m.rseg_pos[k0 + j < k1 ? k0 + j : k0];
-        double2 qv[8];
+        for (int c = 0; c + 4 <= SB; c += 4) {
+            const Int4u v = *reinterpret_cast<const Int4u *>(m.rseg_pos + k0 + c);
+            raw[c] = v.x; raw[c + 1] = v.y; raw[c + 2] = v.z; raw[c + 3] = v.w;
+        }
+        if constexpr (SB % 4 == 2) {
+            const Int2u v = *reinterpret_cast<const Int2u *>(m.rseg_pos + k0 + SB - 2);
+            raw[SB - 2] = v.x; raw[SB - 1] = v.y;
+        }
 #pragma unroll
-        for (int j = 0; j < 8; j++) qv[j] = p.qseg2[ps[j]];
+        for (int j = 0; j < SB; j++) ps[j] = k0 + j < k1 ? raw[j] : raw[0];
+        double2 qv[SB];
 #pragma unroll
-        for (int j = 0; j < 8; j++)
+        for (int j = 0; j < SB; j++) qv[j] = p.qseg2[ps[j]];
+#pragma unroll
+        for (int j = 0; j < SB; j++)
             if (k0 + j < k1) { qsurf += qv[j].x; qsub += qv[j].y; }
     }
     const double qbc = (q.bc < 0) ? m.rqbc[-q.bc] : 0.0;
@@ -828,26 +733,32 @@ shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     if (DIAG) { dg.qriv_down[r] = qdown; dg.qriv_up[r] = qup; dg.qriv_surf[r] = qsurf; dg.qriv_sub[r] = qsub; }
 }
 
-#endif
-
-void launch_river_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int mode,
-                                bool diag, const DevDiag &dg, hipStream_t s) {
-    if (Y.n_own_riv <= 0) return;
+template <int SB>
+static void launch_riv_sb(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int mode, bool diag,
+                          const DevDiag &dg, hipStream_t s) {
     const dim3 grid(((Y.n_own_riv + 255) / 256 + 7) / 8 * 8), blk(256);
+    const int per8 = (int)grid.x / 8;
 #if SHUD_RIV_ABL
     // timing-only ablation build (tools/riv_abl.sh: -DSHUD_RIV_ABL=k); never part of the production library
     if (mode == 0 && !diag) {
-        hipLaunchKernelGGL((shud_riv_kernel_packed<0, false, SHUD_RIV_ABL>), grid, blk, 0, s, m, p, Y, dy, dg, (int)grid.x / 8);
+        hipLaunchKernelGGL((shud_riv_kernel_packed<0, false, SB, SHUD_RIV_ABL>), grid, blk, 0, s, m, p, Y, dy, dg, per8);
         return;
     }
 #endif
     if (mode == 0) {
-        if (diag) hipLaunchKernelGGL((shud_riv_kernel_packed<0, true>), grid, blk, 0, s, m, p, Y, dy, dg, (int)grid.x / 8);
-        else hipLaunchKernelGGL((shud_riv_kernel_packed<0, false>), grid, blk, 0, s, m, p, Y, dy, dg, (int)grid.x / 8);
+        if (diag) hipLaunchKernelGGL((shud_riv_kernel_packed<0, true, SB>), grid, blk, 0, s, m, p, Y, dy, dg, per8);
+        else hipLaunchKernelGGL((shud_riv_kernel_packed<0, false, SB>), grid, blk, 0, s, m, p, Y, dy, dg, per8);
     } else {
-        if (diag) hipLaunchKernelGGL((shud_riv_kernel_packed<1, true>), grid, blk, 0, s, m, p, Y, dy, dg, (int)grid.x / 8);
-        else hipLaunchKernelGGL((shud_riv_kernel_packed<1, false>), grid, blk, 0, s, m, p, Y, dy, dg, (int)grid.x / 8);
+        if (diag) hipLaunchKernelGGL((shud_riv_kernel_packed<1, true, SB>), grid, blk, 0, s, m, p, Y, dy, dg, per8);
+        else hipLaunchKernelGGL((shud_riv_kernel_packed<1, false, SB>), grid, blk, 0, s, m, p, Y, dy, dg, per8);
     }
+}
+
+void launch_river_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int mode,
+                                bool diag, const DevDiag &dg, hipStream_t s) {
+    if (Y.n_own_riv <= 0) return;
+    if (p.riv_sb == 6) launch_riv_sb<6>(m, p, Y, dy, mode, diag, dg, s);
+    else launch_riv_sb<8>(m, p, Y, dy, mode, diag, dg, s);
 }
 
 // ===================================================================================

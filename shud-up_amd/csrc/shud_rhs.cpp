@@ -71,6 +71,20 @@ extern "C" const char *shud_rhs_last_error_string(void) { return g_last_error.c_
 // ---------------------------------------------------------------------------------------------
 // create
 // ---------------------------------------------------------------------------------------------
+// Segments per batch in the river kernel: a wave issues SB flux gathers + its position loads per batch and runs
+// as many batches as its lane with the most segments needs; pick the batch size that issues fewer loads over the
+// owned reaches' 64-reach waves (6 or 8: 16-B + 8-B or two 16-B position loads)
+static int choose_riv_sb(const int *nseg, int nr) {
+    long long cost6 = 0, cost8 = 0;
+    for (int w = 0; w < nr; w += 64) {
+        int mx = 0;
+        for (int r = w; r < nr && r < w + 64; r++) mx = std::max(mx, nseg[r]);
+        cost6 += (long long)((mx + 5) / 6) * (6 + 2);
+        cost8 += (long long)((mx + 7) / 8) * (8 + 2);
+    }
+    return cost6 < cost8 ? 6 : 8;
+}
+
 static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, const std::vector<int> &eflags,
                         const std::vector<int> &seg_off, const std::vector<int> &up_off,
                         const std::vector<int> &up_idx);
@@ -207,6 +221,7 @@ static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, cons
             int r = m->seg_riv[s];
             if (r < h->n_own_riv) rseg_pos[fillp[r]++] = pos_of[s];
         }
+        rseg_pos.resize(rseg_pos.size() + 8, 0);   // the river kernel may read a whole 8-position batch past the end
     }
     std::vector<int> up_off(h->n_own_riv + 1, 0), up_idx;
     for (int r = 0; r < NR; r++) {
@@ -347,6 +362,11 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     if ((uint64_t)48 * NE >= (1ull << 32) || (uint64_t)48 * m->num_seg >= (1ull << 32) ||
         (uint64_t)24 * NE + 8ull * m->num_riv >= (1ull << 32))
         return 0;
+    {                                                               // 16-bit segment count in the reach index word
+        std::vector<int> cnt(m->num_riv, 0);
+        for (int s = 0; s < m->num_seg; s++)
+            if (++cnt[m->seg_riv[s]] > 0xffff) return 0;
+    }
     for (int i = 0; i < NE; i++) {
         if (!(p->aquifer_depth[i] == m->z_surf[i] - m->z_bottom[i])) return 0;
         const int ibc = m->ibc ? m->ibc[i] : 0;
@@ -540,7 +560,7 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         h->rseg_perm = rorder;
     }
     std::vector<double2> rv(4 * (size_t)NR);
-    std::vector<int4> ri(NR), ru(NR);
+    std::vector<int4> ru(NR);
     const int nor = h->n_own_riv;
     for (int r = 0; r < NR; r++) {
         const int dn = (h->lakeon && m->riv_down[r] <= -4) ? -3 : m->riv_down[r];   // into a lake: outlet formula
@@ -552,25 +572,20 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         rv[4 * (size_t)r + 1] = make_double2(m->riv_length[r], m->riv_bed_slope[r]);
         rv[4 * (size_t)r + 2] = make_double2(m->riv_dist2down[r], m->riv_avg_rough[r]);
         rv[4 * (size_t)r + 3] = make_double2(m->riv_depth[r], ib);
-        ri[r] = make_int4(dn, bc, rstart[r], rcnt[r]);
-        int4 u = make_int4(0, 0, 0, 0);
+        int4 u = make_int4(rstart[r], rcnt[r], 0, 0);                // rv_u (shud_dev.h); ghosts: segments only
         if (r < nor) {
             const int n = up_off[r + 1] - up_off[r];
-            if (n <= 3) {
-                int v[3] = {0, 0, 0};
-                for (int k = 0; k < n; k++) v[k] = up_idx[up_off[r] + k];
-                u = make_int4(v[0], v[1], v[2], n);
-            } else {
-                u = make_int4(0, 0, 0, -1);
-            }
+            u = n <= 2 ? make_int4(rstart[r], rcnt[r] | (n << 16), n > 0 ? up_idx[up_off[r]] : 0,
+                                   n > 1 ? up_idx[up_off[r] + 1] : 0)
+                       : make_int4(rstart[r], rcnt[r] | (3 << 16), up_off[r], n);
         }
         ru[r] = u;
     }
-    double2 *rv_d; int4 *ri_d, *ru_d;
+    double2 *rv_d; int4 *ru_d;
     if ((rc = h->upload(&rv_d, rv.data(), rv.size()))) return rc;
-    if ((rc = h->upload(&ri_d, ri.data(), NR))) return rc;
     if ((rc = h->upload(&ru_d, ru.data(), NR))) return rc;
-    P.rv = rv_d; P.rv_i = ri_d; P.rv_u = ru_d;
+    P.rv = rv_d; P.rv_u = ru_d;
+    P.riv_sb = choose_riv_sb(rcnt.data(), nor);
     h->n_classes = ncls;
     h->packed = true;
     return 0;

@@ -21,7 +21,7 @@ def _write(d, counter, rows):
 def test_pmc_summary_model(tmp_path):
     ne, nr, ns = 1000, 100, 500
     c_ele = 164 * ne + 20 * ns
-    c_riv = 104 * nr + 4 * ns
+    c_riv = 88 * nr + 4 * ns
     ele = "void shud::shud_ele_kernel_packed<0, false>(x)"
     riv = "void shud::shud_riv_kernel_packed<0, false, 0>(x)"
     # element: coalesced tally C/2 plus 10 KiB of scattered requests; river: C/2 plus 40 KiB; two launches each

@@ -38,8 +38,9 @@ def per_kernel(d, counter):
 # seg_first 4, the three edges' {edge, Dist2Nabor} 48, area 8 per element; per segment {length, Cwr} 16 + its
 # reach index 4 (round 4: the reach's statics are a gathered per-reach record, counted with the scattered part;
 # rounds 1-3 streamed a 48-B segment record)
-# river kernel: its 64-B record, rv_i 16, rv_u 16, stage 8 per reach; segment positions 4 per segment.
-COALESCED = {"shud_ele_kernel": (164, 0, 20), "shud_riv_kernel": (0, 104, 4)}
+# river kernel: its 64-B record, the 16-B index word rv_u, stage 8 per reach (round 4; rounds 1-3 also rv_i 16);
+# segment positions 4 per segment.
+COALESCED = {"shud_ele_kernel": (164, 0, 20), "shud_riv_kernel": (0, 88, 4)}
 
 
 def main():
