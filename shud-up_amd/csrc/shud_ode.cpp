@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -28,6 +29,12 @@
 #include "shud_handle.h"
 #include "shud_ode.h"
 #include "shud_ode_dev.h"
+
+// SHUD_ODE_SPIN: a fetch polls the last finalize's completion word in host-mapped memory instead of blocking in
+// hipStreamSynchronize (A/B)
+#ifndef SHUD_ODE_SPIN
+#define SHUD_ODE_SPIN 0
+#endif
 
 using namespace shud::ode;
 
@@ -91,6 +98,12 @@ struct shud_ode {
     double *d_part = nullptr, *d_ds = nullptr, *h_ds = nullptr;
     Red red{};
     Red rs(int slot) const { Red r = red; r.slot0 = slot; return r; }   // this reduction's result slots
+    uint64_t fin_seq = 0;   // finalizes enqueued so far (each stores its number into h_ds[S_COUNT + 1] last)
+    void fin(int slot, int nacc, unsigned minmask) {
+        Red r = rs(slot);
+        r.seq = ++fin_seq;
+        finalize(r, nacc, minmask, s);
+    }
     // SPGMR host state
     double Hes[kMaxL + 1][kMaxL]{}, gv[2 * kMaxL]{}, yg[kMaxL + 1]{};
     // integrator scalars (cvode_impl.h names)
@@ -121,7 +134,24 @@ struct shud_ode {
     // host view of the scalar slots (+ the RHS physics error word): every finalize writes them into host-mapped
     // memory (shud_ode_kernels.hip k_finalize), so a fetch is one stream synchronize
     bool fetch() {
-        hipError_t e = hipStreamSynchronize(s);
+        hipError_t e = hipSuccess;
+#if SHUD_ODE_SPIN
+        // poll the last enqueued finalize's completion word (host-mapped, coherent) instead of blocking in the
+        // runtime; after ~2 s, or with no finalize yet, synchronize (which also reports a device fault)
+        bool done = false;
+        if (fin_seq > 0) {
+            const uint64_t *w = reinterpret_cast<const uint64_t *>(h_ds + S_COUNT + 1);
+            const auto t0 = std::chrono::steady_clock::now();
+            for (uint32_t k = 1;; k++) {
+                if (__atomic_load_n(w, __ATOMIC_ACQUIRE) >= fin_seq) { done = true; break; }
+                if ((k & 4095u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
+                __builtin_ia32_pause();
+            }
+        }
+        if (!done) e = hipStreamSynchronize(s);
+#else
+        e = hipStreamSynchronize(s);
+#endif
         if (e == hipSuccess) e = hipGetLastError();
         n_sync++;
         if (e != hipSuccess) {
@@ -316,14 +346,14 @@ struct shud_ode {
         Coefs none{};
         if (bnorm <= deltar) {                                       // cvLsSolve: small rhs
             newton_update(n, nullptr, n, 0, none, curiter > 0 ? nullptr : delta, ewt, acor, take_lazy(), rs(S_DEL), s);
-            finalize(rs(S_DEL), 2, 0u, s);
+            fin(S_DEL, 2, 0u);
             return fetch() ? 0 : -1;
         }
         const double delta_tol = deltar * nrmfac;
         const double r_norm = std::sqrt(h_ds[S_RES]), beta = r_norm;
         if (r_norm <= delta_tol) {                                   // SPGMR: x = x0 = 0
             newton_update(n, nullptr, n, 0, none, nullptr, ewt, acor, take_lazy(), rs(S_DEL), s);
-            finalize(rs(S_DEL), 2, 0u, s);
+            fin(S_DEL, 2, 0u);
             return fetch() ? 0 : -1;
         }
         double rho = beta, rotation_product = 1.0;
@@ -331,7 +361,7 @@ struct shud_ode {
         for (int i = 0; i <= maxl; ++i)
             for (int j = 0; j < maxl; ++j) Hes[i][j] = 0.0;
         krylov_v0(n, delta, ewt, 1.0 / r_norm, VV(0), rs(S_SIG), s);
-        finalize(rs(S_SIG), 1, 0u, s);
+        fin(S_SIG, 1, 0u);
         int rv = LS_CONV_FAIL;
         for (int ll = 0; ll < maxl; ++ll) {
             nl++;
@@ -342,16 +372,16 @@ struct shud_ode {
             nfeDQ++;
             njtimes++;
             atimes(n, VV(ll + 1), ftemp, VV(ll), ewt, VV(0), -gamma, d_ds, rs(S_W), s);                    // [S_W, S_H0] = [||w||^2, V[0].w]
-            finalize(rs(S_W), 2, 0u, s);
+            fin(S_W, 2, 0u);
             // SUNModifiedGS: w -= h[i-1] V[i-1] fused with h[i] = V[i].w; last pass gives the new ||w||^2
             int hs = S_H0;                                           // slot of h[i-1]
             for (int i = 1; i <= ll; ++i) {
                 mgs(n, VV(ll + 1), VV(i - 1), d_ds, hs, VV(i), rs(S_H0 + i), s);
-                finalize(rs(S_H0 + i), 1, 0u, s);
+                fin(S_H0 + i, 1, 0u);
                 hs = S_H0 + i;
             }
             mgs(n, VV(ll + 1), VV(ll), d_ds, hs, nullptr, rs(S_WN), s);
-            finalize(rs(S_WN), 1, 0u, s);
+            fin(S_WN, 1, 0u);
             if (!fetch()) return -1;
             const double vk_norm = std::sqrt(h_ds[S_W]);
             double new_vk_norm = std::sqrt(h_ds[S_WN]);
@@ -361,7 +391,7 @@ struct shud_ode {
                 double new_norm_2 = 0.0;
                 for (int i = 0; i <= ll; ++i) {
                     mgs(n, VV(ll + 1), nullptr, d_ds, 0, VV(i), rs(S_R0 + i), s);
-                    finalize(rs(S_R0 + i), 1, 0u, s);
+                    fin(S_R0 + i, 1, 0u);
                     if (!fetch()) return -1;
                     const double np = h_ds[S_R0 + i];
                     if (np == 0.0) continue;
@@ -401,7 +431,7 @@ struct shud_ode {
             rho = std::fabs(rotation_product * r_norm);
             if (rho <= delta_tol) { converged = 1; break; }
             normalize(n, VV(ll + 1), 1.0 / Hes[ll + 1][ll], ewt, rs(S_SIG), s);
-            finalize(rs(S_SIG), 1, 0u, s);
+            fin(S_SIG, 1, 0u);
         }
         nli += nl;
         if (rv == LS_QR_FAIL) { ncfl++; return -1; }
@@ -427,7 +457,7 @@ struct shud_ode {
         Coefs c{};
         for (int k = 0; k < krydim; ++k) c.c[k] = yg[k];
         newton_update(n, V, n, krydim, c, nullptr, ewt, acor, take_lazy(), rs(S_DEL), s);
-        finalize(rs(S_DEL), 2, 0u, s);
+        fin(S_DEL, 2, 0u);
         return fetch() ? 0 : -1;
     }
 
@@ -443,7 +473,7 @@ struct shud_ode {
         if (rhs(tn, y, ftemp) != 0) return SHUD_ODE_RHSFUNC_FAIL;
         nfe++;
         residual(n, Z(1), az ? nullptr : acor, ftemp, rl1, -gamma, ewt, delta, rs(S_RES), s);
-        finalize(rs(S_RES), 1, 0u, s);
+        fin(S_RES, 1, 0u);
         if (!fetch()) return SHUD_ODE_RHSFUNC_FAIL;
         return 0;
     }
@@ -595,7 +625,7 @@ struct shud_ode {
         } else {
             complete_step_ewt(n, zn, acor, lc, q, copy_to, 0, rtol, atol, ewt_alt, rs(S_EWTMIN), s);
         }
-        finalize(rs(S_EWTMIN), 2, 1u, s);
+        fin(S_EWTMIN, 2, 1u);
         ewt_pending = true;
         ewt_fin_sync = n_sync;
         // cvPrepareNextStep
@@ -623,7 +653,7 @@ struct shud_ode {
             const bool pq = qm1 && pend.acor && q >= 1 && q <= pend.q;
             eta_norms(n, qm1 ? Z(q) : nullptr, qp1 ? Z(qmax) : nullptr, acor, -cquot, ewt, pq ? 1 : 0,
                       pq ? pend.l.c[q] : 0.0, rs(S_ETAQM1), s);
-            finalize(rs(S_ETAQM1), 2, 0u, s);
+            fin(S_ETAQM1, 2, 0u);
             if (!fetch()) return -1;
         }
         if (qm1) {
@@ -704,7 +734,7 @@ struct shud_ode {
         }
         materialize0();
         ewt_set(n, Z(0), ewt, rtol, atol, rs(S_EWTMIN), s);
-        finalize(rs(S_EWTMIN), 2, 1u, s);
+        fin(S_EWTMIN, 2, 1u);
         if (!fetch()) return -1;
         return h_ds[S_EWTMIN] <= 0.0 ? 1 : 0;
     }
@@ -861,8 +891,8 @@ static int ode_alloc(shud_ode *o, double t0, const double *y0, int where, const 
     HIP_TRY(hipMalloc(&o->d_part, (size_t)kMaxAcc * grid_blocks(n) * sizeof(double)));
     HIP_TRY(hipMalloc(&o->d_ds, S_COUNT * sizeof(double)));
     HIP_TRY(hipMemsetAsync(o->d_ds, 0, S_COUNT * sizeof(double), o->s));
-    HIP_TRY(hipHostMalloc(&o->h_ds, (S_COUNT + 1) * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent));
-    memset(o->h_ds, 0, (S_COUNT + 1) * sizeof(double));
+    HIP_TRY(hipHostMalloc(&o->h_ds, (S_COUNT + 2) * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent));
+    memset(o->h_ds, 0, (S_COUNT + 2) * sizeof(double));
     o->red.part = o->d_part;
     o->red.nblk = grid_blocks(n);
     HIP_TRY(hipHostGetDevicePointer((void **)&o->red.hds, o->h_ds, 0));

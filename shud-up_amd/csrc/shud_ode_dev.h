@@ -47,9 +47,11 @@ struct Red {           // partial-sum scratch of one reduction launch and where 
     double *part;      // [kMaxAcc][nblk]
     int nblk;          // blocks of the producing grid, ceil(n / kRedThreads) (fixed per n); also the stride of part
     double *ds;        // device scalar slots [S_COUNT]
-    double *hds;       // host-mapped twin [S_COUNT + 1]; hds[S_COUNT] carries the RHS error word
+    double *hds;       // host-mapped twin [S_COUNT + 2]; hds[S_COUNT] carries the RHS error word, hds[S_COUNT + 1]
+                       // the sequence number of the last finalize done (uint64 bits, stored last, release)
     const uint32_t *err;   // RHS error flags (DevErr::flags) or null
     int slot0;         // first slot of this reduction's results
+    uint64_t seq;      // this finalize's sequence number (host counter)
 };
 
 struct Coefs {         // small host-computed coefficient arrays passed by value

@@ -153,6 +153,11 @@ __global__ void __launch_bounds__(kFinThreads) k_finalize(Red r, int nacc, unsig
         __builtin_memcpy(&w, &fl, sizeof(fl));
         r.hds[S_COUNT] = w;
     }
+    // completion word for a host that polls instead of synchronizing (shud_ode.cpp fetch): thread 0 made every
+    // hds store of this kernel; the release store at system scope orders them before it
+    if (threadIdx.x == 0)
+        __hip_atomic_store(reinterpret_cast<uint64_t *>(r.hds + S_COUNT + 1), r.seq, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 void finalize(const Red &r, int nacc, unsigned minmask, hipStream_t s) {

@@ -69,6 +69,28 @@ def test_heihe(mode, oracle_mod, layout):
 
 
 @pytest.mark.parametrize("mode", [abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP])
+def test_river_junctions(mode, oracle_mod, layout):
+    """Junction shapes of the river kernel's index word (shud_dev.h rv_u): reaches with 0, 1, 2 upstream reaches
+    inline, and 3, 5 and 14 through the up_idx slots (two 8-slot batches).  Headwater reaches of a small synthetic
+    network are rewired into two targets (a headwater is never on a target's downstream path: no cycles);
+    the junction sums keep ascending upstream order (MD_f.cpp:236-240) like the oracle."""
+    from shud_rhs import synth
+    m = synth.synth_model(20000)
+    down = m.riv_down.astype(np.int64)
+    nup = np.bincount(down[down >= 0], minlength=m.num_riv)
+    heads = np.nonzero(nup == 0)[0]
+    t_big = int(np.nonzero((nup == 0) & (down >= 0))[0][0])        # a headwater with a downstream reach
+    t_three = int(np.nonzero(nup == 1)[0][0])
+    movers = [h for h in heads if h not in (t_big, t_three)]
+    down[movers[:14]] = t_big
+    down[movers[14:16]] = t_three
+    m.riv_down = down.astype(np.int32)
+    nup = np.bincount(down[down >= 0], minlength=m.num_riv)
+    assert nup[t_big] == 14 and nup[t_three] == 3 and {0, 1, 2, 5} <= set(nup.tolist())
+    _compare_sequence(m, cases.states(m, None, 2, seed=21), mode, oracle_mod, label="junctions", layout=layout)
+
+
+@pytest.mark.parametrize("mode", [abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP])
 def test_variant_branches(mode, oracle_mod, layout):
     m, y = cases.variant()
     _compare_sequence(m, [y] + cases.states(m, None, 2, seed=9), mode, oracle_mod, label="variant", layout=layout)
