@@ -128,8 +128,6 @@ struct DevPacked {
 int shud_ele_rcp_mask();
 // whether it reads the per-reach segment records (SHUD_SEG_RREC)
 int shud_ele_seg_rrec();
-// whether the river kernel reads the REC2 reach record (shud_ele_packed.hip SHUD_RIV_REC2)
-int shud_riv_rec2();
 
 struct DevDiag {                     // optional diagnostic outputs (ShudFluxOut), local numbering
     double *qele_surf, *qele_sub, *qele_surf_tot, *qele_sub_tot, *q_infil, *q_exfil, *q_recharge;

@@ -584,31 +584,18 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
 // ===================================================================================
 // river kernel on 16-byte reach records (same physics and order as shud_riv_kernel, shud_kernels.hip)
 // ===================================================================================
-// SHUD_RIV_REC2: record {BottomWidth, bankslope | Length, Dist2DownStream | avgRough, (down, BC | downstream's BC
-// << 16) | BedSlope, depth}: what a reach reads of its downstream reach is one 16-B load (its BC is in the
-// reach's own word); 0: {.. | Length, BedSlope | Dist2DownStream, avgRough | depth, (down, BC)}, two loads
-#ifndef SHUD_RIV_REC2
-#define SHUD_RIV_REC2 0
-#endif
-int shud_riv_rec2() { return SHUD_RIV_REC2; }
 struct RivP {
     double w0, bs, len, slope, d2d, n, depth;
-    int down, bc, dbc;      // dbc: the downstream reach's BC (SHUD_RIV_REC2 only)
+    int down, bc;
 };
 __device__ __forceinline__ int2 rv_ib(double x) { return __builtin_bit_cast(int2, x); }   // (down, BC)
 __device__ __forceinline__ RivP riv_load(const DevPacked &p, int r) {
     const double2 *q = p.rv + 4 * (size_t)r;                  // one 64-B record: a single cache line
     const double2 a = q[0], b = q[1], c = q[2], d = q[3];
-    RivP o;
-#if SHUD_RIV_REC2
-    const int2 ib = rv_ib(c.y);
-    o.w0 = a.x; o.bs = a.y; o.len = b.x; o.d2d = b.y; o.n = c.x; o.slope = d.x; o.depth = d.y;
-    o.down = ib.x; o.bc = (int)(int16_t)(ib.y & 0xffff); o.dbc = ib.y >> 16;
-#else
     const int2 ib = rv_ib(d.y);
+    RivP o;
     o.w0 = a.x; o.bs = a.y; o.len = b.x; o.slope = b.y; o.d2d = c.x; o.n = c.y; o.depth = d.x;
-    o.down = ib.x; o.bc = ib.y; o.dbc = 0;
-#endif
+    o.down = ib.x; o.bc = ib.y;
     return o;
 }
 __device__ __forceinline__ RivGeom riv_geom_p(const RivP &q, double y) { return riv_geom(q.w0, q.bs, q.len, y); }
@@ -671,18 +658,11 @@ shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     double qdown = 0.;
     if (!(ABL & 4)) {
         const int d = q.down >= 0 ? q.down : r;                 // clamped: unconditional loads
-#if SHUD_RIV_REC2
-        const double2 sd = p.rv[4 * (size_t)d + 3];             // {BedSlope, depth} of d
-        double ydg;
-        const double ud = riv_stage_p<MODE>(m, Y, d, q.dbc, &ydg);
-        qdown = riv_down_p(q, ur, g, ud, sd.y, sd.x);
-#else
         const double2 bd = p.rv[4 * (size_t)d + 1], dd = p.rv[4 * (size_t)d + 3];   // same line of d's record
         const int bcd = rv_ib(dd.y).y;
         double ydg;
         const double ud = riv_stage_p<MODE>(m, Y, d, bcd, &ydg);
         qdown = riv_down_p(q, ur, g, ud, dd.x, bd.y);
-#endif
     }
     // junction: QrivUp[down] += -QrivDown[i], i ascending (MD_f.cpp:236-240)
     auto up_term = [&](int u) {

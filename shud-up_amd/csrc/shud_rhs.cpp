@@ -367,9 +367,6 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         for (int s = 0; s < m->num_seg; s++)
             if (++cnt[m->seg_riv[s]] > 0xffff) return 0;
     }
-    if (shud_riv_rec2() && m->riv_bc)                                // 16-bit BC columns in the reach record
-        for (int r = 0; r < m->num_riv; r++)
-            if (m->riv_bc[r] < -32768 || m->riv_bc[r] > 32767) return 0;
     for (int i = 0; i < NE; i++) {
         if (!(p->aquifer_depth[i] == m->z_surf[i] - m->z_bottom[i])) return 0;
         const int ibc = m->ibc ? m->ibc[i] : 0;
@@ -565,27 +562,16 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     std::vector<double2> rv(4 * (size_t)NR);
     std::vector<int4> ru(NR);
     const int nor = h->n_own_riv;
-    const bool rec2 = shud_riv_rec2() != 0;
     for (int r = 0; r < NR; r++) {
         const int dn = (h->lakeon && m->riv_down[r] <= -4) ? -3 : m->riv_down[r];   // into a lake: outlet formula
         const int bc = m->riv_bc ? m->riv_bc[r] : 0;
-        double ib;                                                   // (down, BC) packed into one slot
-        if (rec2) {                                                  // + the downstream's BC (shud_riv_rec2)
-            const int dbc = (dn >= 0 && m->riv_bc) ? m->riv_bc[dn] : 0;
-            const int32_t two[2] = {dn, (int32_t)(((uint32_t)(uint16_t)(int16_t)bc) | ((uint32_t)dbc << 16))};
-            memcpy(&ib, two, sizeof ib);
-            rv[4 * (size_t)r + 0] = make_double2(m->riv_bottom_width[r], m->riv_bankslope[r]);
-            rv[4 * (size_t)r + 1] = make_double2(m->riv_length[r], m->riv_dist2down[r]);
-            rv[4 * (size_t)r + 2] = make_double2(m->riv_avg_rough[r], ib);
-            rv[4 * (size_t)r + 3] = make_double2(m->riv_bed_slope[r], m->riv_depth[r]);
-        } else {
-            const int32_t two[2] = {dn, bc};
-            memcpy(&ib, two, sizeof ib);
-            rv[4 * (size_t)r + 0] = make_double2(m->riv_bottom_width[r], m->riv_bankslope[r]);
-            rv[4 * (size_t)r + 1] = make_double2(m->riv_length[r], m->riv_bed_slope[r]);
-            rv[4 * (size_t)r + 2] = make_double2(m->riv_dist2down[r], m->riv_avg_rough[r]);
-            rv[4 * (size_t)r + 3] = make_double2(m->riv_depth[r], ib);
-        }
+        double ib;                                                   // (down, BC) packed into the 4th slot
+        const int32_t two[2] = {dn, bc};
+        memcpy(&ib, two, sizeof ib);
+        rv[4 * (size_t)r + 0] = make_double2(m->riv_bottom_width[r], m->riv_bankslope[r]);
+        rv[4 * (size_t)r + 1] = make_double2(m->riv_length[r], m->riv_bed_slope[r]);
+        rv[4 * (size_t)r + 2] = make_double2(m->riv_dist2down[r], m->riv_avg_rough[r]);
+        rv[4 * (size_t)r + 3] = make_double2(m->riv_depth[r], ib);
         int4 u = make_int4(rstart[r], rcnt[r], 0, 0);                // rv_u (shud_dev.h); ghosts: segments only
         if (r < nor) {
             const int n = up_off[r + 1] - up_off[r];
