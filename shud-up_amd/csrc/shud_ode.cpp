@@ -30,10 +30,10 @@
 #include "shud_ode.h"
 #include "shud_ode_dev.h"
 
-// SHUD_ODE_SPIN: a fetch polls the last finalize's completion word in host-mapped memory instead of blocking in
-// hipStreamSynchronize (A/B)
+// SHUD_ODE_SPIN (default): a fetch polls the last finalize's completion word in host-mapped memory instead of
+// blocking in hipStreamSynchronize (0: synchronize; A/B 4.39 vs 4.43 ms per step, profiles/r04/ode_spin/)
 #ifndef SHUD_ODE_SPIN
-#define SHUD_ODE_SPIN 0
+#define SHUD_ODE_SPIN 1
 #endif
 
 using namespace shud::ode;
