@@ -60,31 +60,84 @@ def shared_partition(gm, world, rank, dist=None, device="cpu"):
 FATAL_FLAGS = 0x01 | 0x02 | 0x04 | 0x08 | 0x80   # SHUD_EF_NAN_QELE | EFFKH | ET_NEG | ET_NAN | HALO_WAIT (shud_rhs.h)
 
 
+# ---- phase heartbeats and watchdogs (the first N > 1 run must end in a number or a named failure) -------------
+# Every rank announces each phase on stderr ("[bench-hb] rank R phase P bound B") and, at N > 1, arms a C-level
+# watchdog (faulthandler: its own thread, no GIL needed, so it fires inside a stuck RCCL / HIP / c10d call too)
+# that dumps every thread's stack and exits the rank with status 1 once the phase outlives its bound.  Under
+# torch.distributed.run that ends the job (the agent stops the other ranks); under bench.py's own launcher the
+# parent also tracks every rank's last phase and enforces the bound plus a grace period itself, terminating all
+# ranks and naming the stuck rank and phase.  Bounds: generous (a fresh box's first `import torch` can take 1-2
+# min), scaled by SHUD_BENCH_PHASE_SCALE (tests).
+PHASE_BOUND_S = {"start": 420, "init": 240, "mesh": 300, "partition": 360, "handle": 240, "settle": 180,
+                 "timed": 180, "parity": 360, "report": 120, "side": 900, "dry_hang": 60}
+HB_TAG = "[bench-hb]"
+
+
+def phase_bound(phase):
+    return PHASE_BOUND_S.get(phase, 300) * float(os.environ.get("SHUD_BENCH_PHASE_SCALE", "1"))
+
+
+def heartbeat(phase, rank, arm):
+    """announce `phase` on stderr; with arm, (re)arm the in-rank watchdog for this phase's bound"""
+    b = phase_bound(phase)
+    print(f"{HB_TAG} rank {rank} phase {phase} bound {b:g}", file=sys.stderr, flush=True)
+    if arm:
+        import faulthandler
+        faulthandler.dump_traceback_later(b, exit=True, file=sys.stderr)
+
+
 def launch_ranks(nproc, argv, dry):
     """`--gpus N > 1` without a launcher: start the N rank processes here (one per GPU, RANK / LOCAL_RANK /
     WORLD_SIZE / MASTER_* in their environment, rendezvous on 127.0.0.1) BEFORE anything touches the GPU, forward
-    the ranks' stdout (rank 0's JSON line) and exit with the first non-zero rank status (the others are then
-    terminated).  This process never initialises HIP."""
+    the ranks' stdout (rank 0's JSON line) and stderr, and exit with the first non-zero rank status (the others are
+    then terminated), naming the rank and the phase it was in.  A watchdog ends the launch when a rank stays in one
+    phase longer than its bound + SHUD_BENCH_GRACE_S (default 60 s): every rank is terminated (SIGTERM, SIGKILL
+    10 s later) and the launch exits 124.  This process never initialises HIP."""
+    import signal
     import socket
     import subprocess
     import threading
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
+    grace = float(os.environ.get("SHUD_BENCH_GRACE_S", "60"))
     procs, outs = [], []
+    phase = [("start", time.monotonic())] * nproc
+    lock = threading.Lock()
     for r in range(nproc):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc), LOCAL_WORLD_SIZE=str(nproc),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SHUD_BENCH_LAUNCHED="1")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
-                                      stdout=subprocess.PIPE, text=True))
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
         outs.append([])
 
-    def pump(k):
+    def pump_out(k):
         for line in procs[k].stdout:
             outs[k].append(line)
-    th = [threading.Thread(target=pump, args=(k,), daemon=True) for k in range(nproc)]
+
+    def pump_err(k):
+        for line in procs[k].stderr:
+            if line.startswith(HB_TAG):
+                f = line.split()
+                with lock:
+                    phase[k] = (f[4], time.monotonic())
+            sys.stderr.write(line)
+            sys.stderr.flush()
+    th = [threading.Thread(target=fn, args=(k,), daemon=True) for k in range(nproc) for fn in (pump_out, pump_err)]
     for t in th:
         t.start()
+
+    def stop_all(live):
+        for j in live:
+            procs[j].send_signal(signal.SIGTERM)
+        t_end = time.monotonic() + 10
+        for j in live:
+            try:
+                procs[j].wait(timeout=max(0.1, t_end - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                procs[j].kill()
+                procs[j].wait()
+
     rc = 0
     live = set(range(nproc))
     while live:
@@ -95,10 +148,25 @@ def launch_ranks(nproc, argv, dry):
             live.discard(k)
             if st != 0 and rc == 0:
                 rc = st if st > 0 else 128 - st
-                print(f"[bench] rank {k} exited with status {st}: stopping the other ranks", file=sys.stderr,
-                      flush=True)
-                for j in live:
-                    procs[j].terminate()
+                with lock:
+                    ph = phase[k][0]
+                print(f"[bench] rank {k} exited with status {st} in phase {ph!r}: stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                stop_all(sorted(live))
+        if rc == 0 and live:
+            now = time.monotonic()
+            with lock:
+                late = [(k, phase[k][0], now - phase[k][1]) for k in sorted(live)
+                        if now - phase[k][1] > phase_bound(phase[k][0]) + grace]
+            if late:
+                k, ph, el = late[0]
+                print(f"[bench] watchdog: rank {k} stuck in phase {ph!r} for {el:.0f} s (bound "
+                      f"{phase_bound(ph):g} s + {grace:g} s grace); terminating all {nproc} ranks "
+                      f"(last phases: {', '.join(f'rank {j}: {phase[j][0]}' for j in range(nproc))})",
+                      file=sys.stderr, flush=True)
+                stop_all(sorted(live))
+                live.clear()
+                rc = 124
         time.sleep(0.05)
     for t in th:
         t.join(timeout=5)
@@ -145,11 +213,22 @@ def main():
     if world != args.gpus:
         print(f"[bench] error: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr, flush=True)
         sys.exit(2)
+    # the in-rank watchdog: on at N > 1 (SHUD_BENCH_RANK_WATCHDOG=0 leaves only the launcher's, tests), off at N = 1
+    arm = world > 1 and os.environ.get("SHUD_BENCH_RANK_WATCHDOG", "1") != "0"
+    hb = lambda phase: heartbeat(phase, rank, arm)            # noqa: E731
+    hb("start")
     if args.dry_launch:
         print(json.dumps({"dry_launch": True, "rank": rank, "world_size": world, "local_rank": local,
                           "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}"}), flush=True)
         if os.environ.get("SHUD_BENCH_DRY_FAIL_RANK") == str(rank):    # launcher test: a failing rank
             sys.exit(5)
+        if os.environ.get("SHUD_BENCH_DRY_HANG_RANK") == str(rank):    # launcher test: a rank that never returns
+            hb("dry_hang")
+            while True:
+                time.sleep(1)
+        if arm:
+            import faulthandler
+            faulthandler.cancel_dump_traceback_later()
         return
     # stdout carries exactly one JSON line: libraries that print banners on it (RCCL prints its version block
     # at communicator init) write to stderr instead until the line is printed
@@ -161,11 +240,13 @@ def main():
     import torch.distributed as dist
     from shud_rhs import abi, partition, runtime, synth, workload
 
+    hb("init")
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     mode = abi.SHUD_MODE_SERIAL if args.mode == "serial" else abi.SHUD_MODE_OMP
 
+    hb("mesh")
     t0 = time.time()
     gm = synth.synth_model(args.n_ele)
     gm.step = workload.random_step_inputs(gm)
@@ -178,6 +259,7 @@ def main():
         # the C++ partitioner + planner (include/shud_partition.h): multilevel and RCB, the smaller largest
         # halo wins; rank 0 partitions (deterministic: any rank would get the same parts) and broadcasts the
         # element -> part map, then every rank builds only its own plan
+        hb("partition")
         tp = time.time()
         ele_part, pst = shared_partition(gm, world, rank, dist if world > 1 else None, f"cuda:{local}")
         cut_e, cut_s = pst["edge_cut"], pst["segment_cut"]
@@ -191,6 +273,7 @@ def main():
         if world > 1:
             dist.broadcast_object_list(uid, src=0)
         part.nccl_unique_id = uid[0]
+        hb("handle")                       # ncclCommInitRank inside
         h = runtime.RhsHandle(lm, mode=mode, device=local, stream=stream.cuda_stream, partition=part)
         y_loc = partition.local_state(y_glob, gm, part)
         model = lm
@@ -210,6 +293,7 @@ def main():
     # GPU goes through in its first ~20 ms of load (element kernel 0.62 -> 0.74 -> 0.62 ms, profiles/r02/kt) then
     # falls outside the K timed evals instead of inside a short K = 20 window
     sp = stream_probe(local) if world == 1 else {}
+    hb("settle")
     ts = time.perf_counter()
     for _ in range(args.settle):
         h.eval_device(0.0, yp, dyp)
@@ -224,27 +308,45 @@ def main():
     # (tools/rank_timing.py: 0.105 ms with events on every eval vs 0.089 without), so N > 1 samples 1 in 4
     t_stride = (4 if (world > 1 or args.partition_1) else 2) if args.steps >= 10 else 1
     h.timing(args.steps, t_stride)
+    hb("timed")
+    # the K timed evals, bracketed by a barrier + synchronize.  Each rank also brackets them with HIP events on its
+    # compute stream (torch's current stream = the handle's stream; every eval's last kernel runs there after its
+    # halo arrived): at N > 1 the value is timed from the slowest rank's event span, so the trailing barrier (and
+    # the ranks' skew leaving it) stays outside the measured window; the barrier-inclusive wall time is reported
+    # beside it.  N = 1: the wall time between the two synchronizes.
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
+    ev0.record()
     for k in range(args.steps):
         h.eval_device(0.0, yp, dyp)
+    ev1.record()
     torch.cuda.synchronize()
+    dt_rank_wall = time.perf_counter() - t_start
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    dt = time.perf_counter() - t_start
+    dt_wall = time.perf_counter() - t_start
+    dt_ev = ev0.elapsed_time(ev1) * 1e-3
+    dt = dt_wall
     ms_ele_loop, ms_riv_loop, ms_eval_loop, n_timed = h.timing_read()
     kmax = None
+    timing_detail = None
     if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        tt = torch.tensor([dt_ev, dt_rank_wall, dt_wall], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+        dt = float(tt[0])
+        timing_detail = {"source": "max over ranks of each rank's HIP-event span of the K evals on its compute stream",
+                         "ms_per_step_events_max": float(tt[0]) / args.steps * 1e3,
+                         "ms_per_step_rank_wall_max": float(tt[1]) / args.steps * 1e3,
+                         "ms_per_step_wall_incl_barrier": float(tt[2]) / args.steps * 1e3}
         # the slowest rank's in-loop kernel times (each rank's HIP events on its own compute stream)
         kt = torch.tensor([ms_ele_loop, ms_riv_loop, ms_eval_loop], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(kt, op=dist.ReduceOp.MAX)
         kmax = {"shud_ele_kernel": float(kt[0]), "shud_riv_kernel": float(kt[1]), "eval": float(kt[2])}
+    hb("report")
     # a fatal error flag (NaN fluxes, effKH range, ET checks, a timed-out halo poll) means the timed evals computed
     # wrong DY: no throughput line, non-zero exit on every rank
     err = h.get_error()
@@ -259,9 +361,11 @@ def main():
         sys.exit(3)
     parity = None
     if (world > 1 or args.partition_1) and not args.no_parity:
+        hb("parity")
         parity = parity_vs_1gpu(h, gm, y_glob, part, mode, local, stream, yp, dyp, dy_t, dist if world > 1 else None)
         if not parity["ok"]:
             print(f"[bench] rank {rank}: DY differs from the single-GPU handle: {parity}", file=sys.stderr, flush=True)
+        hb("report")
 
     # per-kernel times: HIP events recorded inside the timed loop on the handle's stream (= torch's current
     # stream); a partitioned handle also gets a serialized per-phase breakdown (halo exchange alone)
@@ -326,6 +430,8 @@ def main():
         },
         "cpu_baseline": None,
     }
+    if timing_detail:
+        out["timing"] = timing_detail
     if world > 1 or args.partition_1:
         out["rccl_ranks"] = world
         out["parity_vs_1gpu"] = None if parity is None else parity["all_ok"]
@@ -344,9 +450,12 @@ def main():
         out["roofline"].update(tr)
         if out["roofline"].get("traffic"):
             out["roofline"]["frac_actual"] = out["roofline"]["traffic"] / (ms_ele * 1e-3) / HBM_PEAK
-            if sp:   # measured bytes against the measured copy ceiling (the canonical count exceeds the bytes moved)
+            if sp:   # measured bytes against the measured ceilings (the canonical count exceeds the bytes moved)
                 out["roofline"]["frac_of_stream_copy_actual"] = (out["roofline"]["traffic"] / (ms_ele * 1e-3) / 1e9
                                                                  / sp["stream_copy_GBs"])
+                # the element kernel reads ~4x what it writes: its fairest ceiling is the box's read-only rate
+                out["roofline"]["frac_of_stream_read_actual"] = (out["roofline"]["traffic"] / (ms_ele * 1e-3) / 1e9
+                                                                 / sp["stream_read_GBs"])
         rt = tr.get("riv_traffic")
         if rt and ms_riv > 0:
             out["roofline"]["riv_frac_actual"] = rt / (ms_riv * 1e-3) / HBM_PEAK
@@ -360,6 +469,7 @@ def main():
             print(f"[bench] {key} failed: {e!r}", file=sys.stderr, flush=True)
             out[key] = {"error": repr(e)}
 
+    hb("side")
     if not args.no_host_vectors and world == 1:
         def host_vectors():
             y_h = np.ascontiguousarray(y_loc)
@@ -407,8 +517,12 @@ def main():
         os.write(json_fd, (json.dumps(out) + "\n").encode())
     if h is not None:
         h.close()
+    hb("report")
     if world > 1:
         dist.destroy_process_group()
+    if arm:
+        import faulthandler
+        faulthandler.cancel_dump_traceback_later()
 
 
 def parity_vs_1gpu(h, gm, y_glob, part, mode, local, stream, yp, dyp, dy_t, dist, calls=2):

@@ -86,7 +86,9 @@ int shud_ode_solve(shud_ode_t o, double tout, double *y_out, int where, double *
 int shud_ode_get_dky(shud_ode_t o, double t, int k, double *dky, int where);
 int shud_ode_get_stats(shud_ode_t o, ShudOdeStats *st);
 /* device pointer of the current Nordsieck zn[0] (y at tcur), NY doubles; valid until the next solve; read-only
- * (the integrator keeps the next step's error weights, computed from this zn[0] at the end of the last step) */
+ * (the integrator keeps the next step's error weights, computed from this zn[0] at the end of the last step).
+ * Complete on return: a deferred completion of zn[0] is applied and the integrator's stream is synchronized, so
+ * any stream may read it (NULL on a device error). */
 const double *shud_ode_state_device(shud_ode_t o);
 int shud_ode_destroy(shud_ode_t o);
 

@@ -119,6 +119,12 @@ struct DevPacked {
     // that many upstream reaches, in w2, w3; code 3 = more, up_idx[w2 .. w2 + w3) (ascending global order)
     const int4 *rv_u;
     int riv_sb;             // segments per batch in the river kernel (6 or 8; choose_riv_sb)
+    // QrivDown of every local reach (owned and ghost), computed once per eval by workgroups appended to the last
+    // element launch (it depends on y only, MD_f.cpp:41-43); the river kernel then reads a reach's own QrivDown and
+    // each upstream reach's from here (MD_f.cpp:236-240) instead of recomputing them from the reach records.
+    // nullptr: off (SHUD_RHS_QD=0), the river kernel recomputes them
+    double *qdown;          // [nqd]
+    int nqd;
     int lds_big;            // 1: 129..kLdsClassMaxBig classes take the 1024-thread LDS-table kernel (host dispatch)
     // correctly rounded reciprocals of static geometric divisors, uploaded only for a kernel built with the
     // matching SHUD_RCP bit (shud_ele_rcp_mask()): 1 area, 2 Dist2Nabor [3][NE], 4 segment reach BedThick
@@ -173,9 +179,12 @@ struct YView {
 
 void launch_element_kernel(const DevMesh &m, const YView &Y, double *dy, int n_compute, int cur, int cur_e,
                            int mode, bool open, bool diag, const DevDiag &dg, hipStream_t s, int variant = 0);
-void launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1,
+// with_qd: append the QrivDown workgroups (DevPacked::qdown) to this launch — only the last element launch of an
+// eval, which runs after the halo; returns whether they were appended (the river kernel then reads the slots)
+bool launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1,
                                   int cur, int mode, bool open, bool diag, bool fu_unit, const DevDiag &dg,
-                                  hipStream_t s, const DevLake *lake = nullptr, bool interior = false);
+                                  hipStream_t s, const DevLake *lake = nullptr, bool interior = false,
+                                  bool with_qd = false);
 // partitioned handles: the boundary + ghost elements [n_int, n_all) ride at the end of the interior element launch;
 // their workgroups wait until the comm stream has published the halo (flag >= epoch; epoch 0 = stream-ordered)
 struct HaloWait {
@@ -185,14 +194,15 @@ struct HaloWait {
 };
 bool launch_element_kernel_packed_fold(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int n_int,
                                        int n_all, int cur, int mode, bool open, bool fu_unit, const DevDiag &dg,
-                                       const HaloWait &hw, hipStream_t s);
+                                       const HaloWait &hw, hipStream_t s, bool with_qd = false);
 void launch_halo_flag(unsigned long long *flag, unsigned long long epoch, hipStream_t s);
 // test hooks (shud_rhs_debug_halo): a one-lane spin of `ticks` wall-clock ticks, and a plain vector copy (the
 // stand-in for RCCL's receive kernels writing the ghost buffers), both on the comm stream
 void launch_spin(unsigned long long ticks, hipStream_t s);
 void launch_copy_f64(double *dst, const double *src, size_t n, hipStream_t s);
+// qd: the eval's element launch wrote DevPacked::qdown
 void launch_river_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int mode,
-                                bool diag, const DevDiag &dg, hipStream_t s);
+                                bool diag, const DevDiag &dg, hipStream_t s, bool qd = false);
 void launch_lake_kernel(const DevMesh &m, const DevPacked &p, const DevLake &L, const YView &Y, double *dy,
                         bool diag, const DevDiag &dg, hipStream_t s);
 void launch_pack_step_kernel(const DevMesh &m, const DevPacked &p, int n, int cur, unsigned what, hipStream_t s);

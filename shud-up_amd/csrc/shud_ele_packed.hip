@@ -158,7 +158,26 @@ __device__ __forceinline__ void tab_store(const DevPacked &p, const double (&tv)
 }
 // workgroup -> tile: XCD-contiguous chunks (block_id<1>, shud_physics.h) with the chunk length per8 = grid/8
 // passed by the launcher, so no workgroup reads the grid size from the dispatch packet at its start
-__device__ __forceinline__ int tile_of(int per8) { return (int)(blockIdx.x & 7) * per8 + (int)(blockIdx.x >> 3); }
+__device__ __forceinline__ int tile_of(int per8, int b) { return (b & 7) * per8 + (b >> 3); }
+__device__ __forceinline__ int tile_of(int per8) { return tile_of(per8, (int)blockIdx.x); }
+
+// QrivDown pre-pass (DevPacked::qdown): nb_q workgroups of the last element launch of an eval compute every local
+// reach's QrivDown (MD_RiverFlux.cpp:5-63; a function of y only, computed once per reach as MD_f.cpp:41-43 does)
+// into an 8-B slot, so the river kernel reads its own and its upstream reaches' values (MD_f.cpp:236-240) instead
+// of recomputing each from a 64-B reach record and two stages.  They ride after the element tiles, in the launch's
+// tail (SHUD_QD_FIRST=1: before them, A/B); nb_q is a multiple of 8, so the element tiles keep their XCD chunks.
+#ifndef SHUD_QD_FIRST
+#define SHUD_QD_FIRST 0
+#endif
+template <int MODE>
+__device__ __forceinline__ void qd_pre(const DevMesh &m, const DevPacked &p, const YView &Y, int r);
+// the QrivDown block index of this workgroup, or -1 for an element workgroup
+__device__ __forceinline__ int qd_block(int nb_e, int nb_q) {
+    const int b = (int)blockIdx.x;
+    if (SHUD_QD_FIRST) return b < nb_q ? b : -1;
+    return b >= nb_e ? b - nb_e : -1;
+}
+__device__ __forceinline__ int ele_block(int nb_q) { return (int)blockIdx.x - (SHUD_QD_FIRST ? nb_q : 0); }
 
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
 __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, const YView &Y, double *__restrict__ dy,
@@ -168,9 +187,17 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
 __global__ void __launch_bounds__(256, SHUD_ELE_WAVES)
 shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int i0, int n_compute, int cur,
-                       DevDiag dg, DevLake lk, int per8) {
+                       DevDiag dg, DevLake lk, int per8, int nb_e, int nb_q) {
     extern __shared__ double lct[];                       // ncls * CF_LDS_STRIDE doubles when LCT
-    const int i = i0 + tile_of(per8) * 256 + (int)threadIdx.x;   // elements [i0, n_compute)
+    if (nb_q) {
+        const int qb = qd_block(nb_e, nb_q);
+        if (qb >= 0) {
+            const int r = qb * 256 + (int)threadIdx.x;
+            if (r < p.nqd) qd_pre<MODE>(m, p, Y, r);
+            return;
+        }
+    }
+    const int i = i0 + tile_of(per8, ele_block(nb_q)) * 256 + (int)threadIdx.x;   // elements [i0, n_compute)
     const bool act = i < n_compute;
     double tv[kTabBatch];
     if (LCT) tab_issue<256>(p, tv);
@@ -229,9 +256,15 @@ __device__ __forceinline__ void halo_wait(const DevMesh &m, const HaloWait &hw, 
 template <int MODE, bool OPEN, bool FU1>
 __global__ void __launch_bounds__(256, SHUD_ELE_WAVES)
 shud_ele_kernel_packed_fold(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int n_int, int n_all, int cur,
-                            DevDiag dg, int per8, int nb_int, HaloWait hw) {
+                            DevDiag dg, int per8, int nb_int, HaloWait hw, int nb_eb) {
     extern __shared__ double lct[];
     const DevLake lk{};
+    if ((int)blockIdx.x >= nb_eb) {                           // QrivDown blocks (after the boundary ones): ghost stages
+        const int r = ((int)blockIdx.x - nb_eb) * 256 + (int)threadIdx.x;
+        halo_wait(m, hw, n_int);
+        if (r < p.nqd) qd_pre<MODE>(m, p, Y, r);
+        return;
+    }
     if ((int)blockIdx.x < nb_int) {
         const int i = tile_of(per8) * 256 + (int)threadIdx.x;
         const bool act = i < n_int;
@@ -626,6 +659,20 @@ __device__ __forceinline__ double riv_down_p(const RivP &q, double uq, const Riv
 __device__ __forceinline__ double riv_down_outlet(const RivP &q, double uq, const RivGeom &g) {
     return riv_down_p(q, uq, g, 0., 0., 0.);
 }
+// QrivDown of local reach r (owned or ghost) into its slot: the river kernel's own-reach term, operand for operand
+// (a ghost reach whose downstream is not local carries the outlet code on its record; its slot is never read)
+template <int MODE>
+__device__ __forceinline__ void qd_pre(const DevMesh &m, const DevPacked &p, const YView &Y, int r) {
+    const RivP q = riv_load(p, r);
+    double yg;
+    const double ur = riv_stage_p<MODE>(m, Y, r, q.bc, &yg);
+    const RivGeom g = riv_geom_p(q, yg);
+    const int d = q.down >= 0 ? q.down : r;                     // clamped: unconditional loads
+    const double2 bd = p.rv[4 * (size_t)d + 1], dd = p.rv[4 * (size_t)d + 3];
+    double ydg;
+    const double ud = riv_stage_p<MODE>(m, Y, d, rv_ib(dd.y).y, &ydg);
+    p.qdown[r] = riv_down_p(q, ur, g, ud, dd.x, bd.y);
+}
 
 // ABL (timing-only ablation builds, -DSHUD_RIV_ABL=k; results are wrong when != 0): bit 0 skips the upstream
 // reaches, bit 1 the segment gathers, bit 2 the downstream reach
@@ -642,7 +689,7 @@ struct __attribute__((packed, aligned(4))) Int2u { int x, y; };
 // together from the offset in that word (no up_off load, no index load per upstream reach); a segment batch's
 // flux positions as 16-B (+ 8-B) loads instead of one 4-B load each; SB segments per batch, chosen by the host
 // from the reaches' segment counts (choose_riv_sb, shud_rhs.cpp).  0.0709 -> 0.0605 ms at syn-10M, same bits.
-template <int MODE, bool DIAG, int SB, int ABL = 0>
+template <int MODE, bool DIAG, int SB, bool QD, int ABL = 0>
 __global__ void __launch_bounds__(256)
 shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, DevDiag dg, int per8) {
     // XCD-chunked workgroup order: a reach's up/downstream records sit a few blocks away in index space,
@@ -656,7 +703,10 @@ shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     const double ur = riv_stage_p<MODE>(m, Y, r, q.bc, &yg);
     const RivGeom g = riv_geom_p(q, yg);
     double qdown = 0.;
-    if (!(ABL & 4)) {
+    if (ABL & 4) {
+    } else if (QD) {
+        qdown = p.qdown[r];                                     // this eval's pre-pass (qd_pre), same operands
+    } else {
         const int d = q.down >= 0 ? q.down : r;                 // clamped: unconditional loads
         const double2 bd = p.rv[4 * (size_t)d + 1], dd = p.rv[4 * (size_t)d + 3];   // same line of d's record
         const int bcd = rv_ib(dd.y).y;
@@ -664,8 +714,11 @@ shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         const double ud = riv_stage_p<MODE>(m, Y, d, bcd, &ydg);
         qdown = riv_down_p(q, ur, g, ud, dd.x, bd.y);
     }
-    // junction: QrivUp[down] += -QrivDown[i], i ascending (MD_f.cpp:236-240)
+    // junction: QrivUp[down] += -QrivDown[i], i ascending (MD_f.cpp:236-240).  An upstream reach u's QrivDown is
+    // the same expression on the same operands (its downstream is r: stage ur, r's depth and slope) whether read
+    // from u's pre-pass slot or recomputed from u's record
     auto up_term = [&](int u) {
+        if (QD) return -p.qdown[u];
         const RivP qu = riv_load(p, u);
         double yu;
         const double uu = riv_stage_p<MODE>(m, Y, u, qu.bc, &yu);
@@ -733,7 +786,7 @@ shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     if (DIAG) { dg.qriv_down[r] = qdown; dg.qriv_up[r] = qup; dg.qriv_surf[r] = qsurf; dg.qriv_sub[r] = qsub; }
 }
 
-template <int SB>
+template <int SB, bool QD>
 static void launch_riv_sb(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int mode, bool diag,
                           const DevDiag &dg, hipStream_t s) {
     const dim3 grid(((Y.n_own_riv + 255) / 256 + 7) / 8 * 8), blk(256);
@@ -741,24 +794,31 @@ static void launch_riv_sb(const DevMesh &m, const DevPacked &p, const YView &Y, 
 #if SHUD_RIV_ABL
     // timing-only ablation build (tools/riv_abl.sh: -DSHUD_RIV_ABL=k); never part of the production library
     if (mode == 0 && !diag) {
-        hipLaunchKernelGGL((shud_riv_kernel_packed<0, false, SB, SHUD_RIV_ABL>), grid, blk, 0, s, m, p, Y, dy, dg, per8);
+        hipLaunchKernelGGL((shud_riv_kernel_packed<0, false, SB, QD, SHUD_RIV_ABL>), grid, blk, 0, s, m, p, Y, dy, dg,
+                           per8);
         return;
     }
 #endif
     if (mode == 0) {
-        if (diag) hipLaunchKernelGGL((shud_riv_kernel_packed<0, true, SB>), grid, blk, 0, s, m, p, Y, dy, dg, per8);
-        else hipLaunchKernelGGL((shud_riv_kernel_packed<0, false, SB>), grid, blk, 0, s, m, p, Y, dy, dg, per8);
+        if (diag) hipLaunchKernelGGL((shud_riv_kernel_packed<0, true, SB, QD>), grid, blk, 0, s, m, p, Y, dy, dg, per8);
+        else hipLaunchKernelGGL((shud_riv_kernel_packed<0, false, SB, QD>), grid, blk, 0, s, m, p, Y, dy, dg, per8);
     } else {
-        if (diag) hipLaunchKernelGGL((shud_riv_kernel_packed<1, true, SB>), grid, blk, 0, s, m, p, Y, dy, dg, per8);
-        else hipLaunchKernelGGL((shud_riv_kernel_packed<1, false, SB>), grid, blk, 0, s, m, p, Y, dy, dg, per8);
+        if (diag) hipLaunchKernelGGL((shud_riv_kernel_packed<1, true, SB, QD>), grid, blk, 0, s, m, p, Y, dy, dg, per8);
+        else hipLaunchKernelGGL((shud_riv_kernel_packed<1, false, SB, QD>), grid, blk, 0, s, m, p, Y, dy, dg, per8);
     }
 }
 
 void launch_river_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int mode,
-                                bool diag, const DevDiag &dg, hipStream_t s) {
+                                bool diag, const DevDiag &dg, hipStream_t s, bool qd) {
     if (Y.n_own_riv <= 0) return;
-    if (p.riv_sb == 6) launch_riv_sb<6>(m, p, Y, dy, mode, diag, dg, s);
-    else launch_riv_sb<8>(m, p, Y, dy, mode, diag, dg, s);
+    const int sb = p.riv_sb;
+    if (qd && p.qdown) {
+        if (sb == 6) launch_riv_sb<6, true>(m, p, Y, dy, mode, diag, dg, s);
+        else launch_riv_sb<8, true>(m, p, Y, dy, mode, diag, dg, s);
+    } else {
+        if (sb == 6) launch_riv_sb<6, false>(m, p, Y, dy, mode, diag, dg, s);
+        else launch_riv_sb<8, false>(m, p, Y, dy, mode, diag, dg, s);
+    }
 }
 
 // ===================================================================================
@@ -879,36 +939,39 @@ static void launch_big(const DevMesh &m, const DevPacked &p, const YView &Y, dou
 
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
 static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1, int cur,
-                     const DevDiag &dg, const DevLake &lk, hipStream_t s) {
+                     const DevDiag &dg, const DevLake &lk, hipStream_t s, int nq = 0) {
     int nb = (i1 - i0 + 255) / 256;
     nb = (nb + 7) / 8 * 8;                  // block_id<1> deals blocks to XCDs in contiguous chunks
+    const int nbq = nq > 0 ? ((nq + 255) / 256 + 7) / 8 * 8 : 0;
     const size_t lds = LCT ? (size_t)p.ncls * CF_LDS_STRIDE * sizeof(double) : 0;
-    hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH>), dim3(nb), dim3(256), lds, s, m, p,
-                       Y, dy, i0, i1, cur, dg, lk, nb / 8);
+    hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH>), dim3(nb + nbq), dim3(256), lds, s,
+                       m, p, Y, dy, i0, i1, cur, dg, lk, nb / 8, nb, nbq);
 }
 
-void launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1,
+bool launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1,
                                   int cur, int mode, bool open, bool diag, bool fu_unit, const DevDiag &dg,
-                                  hipStream_t s, const DevLake *lake, bool interior) {
-    if (i1 <= i0) return;
+                                  hipStream_t s, const DevLake *lake, bool interior, bool with_qd) {
+    if (i1 <= i0) return false;
     DevLake lk{};
     if (lake) lk = *lake;
+    // the QrivDown pre-pass rides in the 256-thread launches (not the 1024-thread big-class one)
+    const int nq = (with_qd && p.qdown && p.nqd > 0 && (lake || p.ncls <= LDS_CLS_MAX)) ? p.nqd : 0;
     // lakes: serial semantics only (the handle rejects OMP + lakes), class table in LDS, with or without ghosts.
     // A partitioned handle's interior elements (interior = true: every lateral neighbour and every segment's
     // reach owned) read only owned state, so they take the ghost-free instantiation (direct y addressing).
     const bool gh = !interior && (Y.gele != nullptr || Y.griv != nullptr);
 #define LP(MO, OP, DI, FU) do {                                                                            \
         if (lake && MO == 0) {                                                                            \
-            if (gh) launch_p<MO, OP, DI, FU, true, true, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s);      \
-            else launch_p<MO, OP, DI, FU, true, true, false>(m, p, Y, dy, i0, i1, cur, dg, lk, s);        \
+            if (gh) launch_p<MO, OP, DI, FU, true, true, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s, nq);  \
+            else launch_p<MO, OP, DI, FU, true, true, false>(m, p, Y, dy, i0, i1, cur, dg, lk, s, nq);    \
         }                                                                                                 \
         else if (p.ncls > LDS_CLS_MAX && p.ncls <= kLdsClassMaxBig && p.lds_big) {                        \
             if (gh) launch_big<MO, OP, DI, FU, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s);                 \
             else launch_big<MO, OP, DI, FU, false>(m, p, Y, dy, i0, i1, cur, dg, lk, s);                   \
         }                                                                                                 \
         else if (p.ncls <= LDS_CLS_MAX) {                                                                 \
-            if (gh) launch_p<MO, OP, DI, FU, true, false, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s);     \
-            else launch_p<MO, OP, DI, FU, true, false, false>(m, p, Y, dy, i0, i1, cur, dg, lk, s);       \
+            if (gh) launch_p<MO, OP, DI, FU, true, false, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s, nq); \
+            else launch_p<MO, OP, DI, FU, true, false, false>(m, p, Y, dy, i0, i1, cur, dg, lk, s, nq);   \
         } else launch_p<MO, OP, DI, FU, false, false, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s); } while (0)
 #define LFU(MO, OP, DI) do { if (fu_unit) LP(MO, OP, DI, true); else LP(MO, OP, DI, false); } while (0)
 #define LDI(MO, OP) do { if (diag) LFU(MO, OP, true); else LFU(MO, OP, false); } while (0)
@@ -918,17 +981,21 @@ void launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YV
 #undef LDI
 #undef LFU
 #undef LP
+    return nq > 0;
 }
 
-// false: this configuration has no folded instantiation (the caller launches interior and boundary separately)
+// false: this configuration has no folded instantiation (the caller launches interior and boundary separately).
+// with_qd: the QrivDown blocks follow the boundary ones (and wait for the halo like them); they always ride here.
 bool launch_element_kernel_packed_fold(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int n_int,
                                        int n_all, int cur, int mode, bool open, bool fu_unit, const DevDiag &dg,
-                                       const HaloWait &hw, hipStream_t s) {
+                                       const HaloWait &hw, hipStream_t s, bool with_qd) {
     if (n_int <= 0 || n_all <= n_int || p.ncls > LDS_CLS_MAX) return false;
     const int nb_int = ((n_int + 255) / 256 + 7) / 8 * 8, nb_b = (n_all - n_int + 255) / 256;
+    const int nbq = (with_qd && p.qdown && p.nqd > 0) ? (p.nqd + 255) / 256 : 0;
     const size_t lds = (size_t)p.ncls * CF_LDS_STRIDE * sizeof(double);
-#define LF(MO, OP, FU) hipLaunchKernelGGL((shud_ele_kernel_packed_fold<MO, OP, FU>), dim3(nb_int + nb_b), dim3(256), lds, \
-                                          s, m, p, Y, dy, n_int, n_all, cur, dg, nb_int / 8, nb_int, hw)
+#define LF(MO, OP, FU) hipLaunchKernelGGL((shud_ele_kernel_packed_fold<MO, OP, FU>), dim3(nb_int + nb_b + nbq), dim3(256), \
+                                          lds, s, m, p, Y, dy, n_int, n_all, cur, dg, nb_int / 8, nb_int, hw,          \
+                                          nb_int + nb_b)
     if (mode == 0) {
         if (open) { if (fu_unit) LF(0, true, true); else LF(0, true, false); }
         else { if (fu_unit) LF(0, false, true); else LF(0, false, false); }

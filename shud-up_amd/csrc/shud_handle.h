@@ -57,6 +57,7 @@ struct shud_rhs {
     DevPacked dp{};
     int n_classes = 0;
     bool fu_unit[2] = {true, true};      // fu_Surf / fu_Sub are all 1.0 (cryosphere off): not read
+    bool qd_now = false;                 // this eval's element launch wrote DevPacked::qdown (river kernel reads it)
 
     // host-pointer eval staging
     double *d_y = nullptr, *d_ydot = nullptr, *d_scratch_dy = nullptr;

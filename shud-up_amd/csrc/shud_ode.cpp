@@ -993,7 +993,12 @@ extern "C" int shud_ode_get_stats(shud_ode_t o, ShudOdeStats *st) {
 
 extern "C" const double *shud_ode_state_device(shud_ode_t o) {
     if (!o) return nullptr;
+    if (hipSetDevice(o->device) != hipSuccess) return nullptr;
     o->materialize0();                 // zn[0]'s completion may still be pending (ode::Pend)
+    if (hipGetLastError() != hipSuccess) return nullptr;
+    // the completion (and anything else the last solve left queued) runs on the integrator's non-blocking stream:
+    // finish it here, so a consumer on another stream or the default stream never reads a stale y(tcur)
+    if (hipStreamSynchronize(o->s) != hipSuccess) return nullptr;
     return o->zn;
 }
 

@@ -194,9 +194,11 @@ void ewt_set(int64_t n, const double *zn0, double *ewt, double rtol, double atol
 // PEND (cvPredict after a deferred cvCompleteStep, Pend): zn[j] = l[j]*acor + zn[j] and zn[j] *= r[j] (j = 1..Q) in
 // registers first — k_complete's and k_rescale's arithmetic — then the Pascal update; zn[Q] is stored too, and
 // zn[copy_to] = acor.  Saves the completion's own pass over zn[1..Q] (+16 B/entry here, -16*Q B/entry there).
+// ycor is not __restrict__: predict_pend passes acor as both ycor and pd.acor, and the eager-fill A/B build
+// (SHUD_ODE_LAZY_YCOR=0) stores ycor[i] after loading pd.acor[i] (the default build never stores ycor)
 template <int Q, bool FWD, bool PEND, int U>
 __global__ void __launch_bounds__(kThreads) k_pascal(int64_t n, double *__restrict__ zn, double *__restrict__ y,
-                                                     double *__restrict__ ycor, Pend pd) {
+                                                     double *ycor, Pend pd) {
     using T = DN<Q + 2>;                  // [0..Q] zn, [Q + 1] acor (PEND)
     one<T>(n, [&](int64_t i) {
         T a;

@@ -586,6 +586,12 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     if ((rc = h->upload(&ru_d, ru.data(), NR))) return rc;
     P.rv = rv_d; P.rv_u = ru_d;
     P.riv_sb = choose_riv_sb(rcnt.data(), nor);
+    if (const char *sb = getenv("SHUD_RIV_SB"); sb && (atoi(sb) == 6 || atoi(sb) == 8)) P.riv_sb = atoi(sb);   // tests
+    // QrivDown pre-pass slots (shud_dev.h DevPacked::qdown); SHUD_RHS_QD=0: the river kernel recomputes (A/B)
+    if (NR > 0 && !(getenv("SHUD_RHS_QD") && getenv("SHUD_RHS_QD")[0] == '0')) {
+        if ((rc = h->upload(&P.qdown, (const double *)nullptr, NR))) return rc;
+        P.nqd = NR;
+    }
     h->n_classes = ncls;
     h->packed = true;
     return 0;
@@ -866,18 +872,24 @@ static void launch_ele(shud_rhs *h, const double *y, double *dy, int cur, int cu
                        int i1 = -1) {
     YView Y{y, h->d_gele, h->d_griv, h->n_own, h->n_own_riv};
     if (i1 < 0) i1 = h->n_own + h->n_segghost;
-    if (h->packed && !h->variant)
-        launch_element_kernel_packed(h->dm, h->dp, Y, dy, i0, i1, cur, h->mode, h->open, diag,
-                                     h->fu_unit[0] && h->fu_unit[1], h->dd, h->stream, h->lakeon ? &h->lk : nullptr,
-                                     h->partitioned && i1 <= h->n_int);
-    else
+    // the last element launch of an eval (after the halo in every partitioned path) carries the QrivDown pre-pass
+    const bool last = i1 == h->n_own + h->n_segghost;
+    if (h->packed && !h->variant) {
+        const bool qd = launch_element_kernel_packed(h->dm, h->dp, Y, dy, i0, i1, cur, h->mode, h->open, diag,
+                                                     h->fu_unit[0] && h->fu_unit[1], h->dd, h->stream,
+                                                     h->lakeon ? &h->lk : nullptr, h->partitioned && i1 <= h->n_int,
+                                                     last);
+        if (last) h->qd_now = qd;
+    } else {
         launch_element_kernel(h->dm, Y, dy, h->n_own + h->n_segghost, cur, cur_e, h->mode, h->open, diag, h->dd,
                               h->stream, h->variant);
+        h->qd_now = false;
+    }
 }
 static void launch_riv(shud_rhs *h, const double *y, double *dy, bool diag) {
     YView Y{y, h->d_gele, h->d_griv, h->n_own, h->n_own_riv};
     if (h->packed && !h->variant)
-        launch_river_kernel_packed(h->dm, h->dp, Y, dy, h->mode, diag, h->dd, h->stream);
+        launch_river_kernel_packed(h->dm, h->dp, Y, dy, h->mode, diag, h->dd, h->stream, h->qd_now);
     else
         launch_river_kernel(h->dm, Y, dy, h->mode, diag, h->dd, h->stream);
     if (h->lakeon) launch_lake_kernel(h->dm, h->dp, h->lk, Y, dy, diag, h->dd, h->stream);
@@ -930,7 +942,8 @@ static int launch_split(shud_rhs *h, const double *y, double *dy, hipEvent_t e_m
         const HaloWait hw{h->d_halo_flag, stream_halo ? 0ull : h->halo_epoch, h->halo_timeout};
         if (launch_element_kernel_packed_fold(h->dm, h->dp, Y, dy, h->n_int, h->n_own + h->n_segghost, h->cur,
                                               h->mode, h->open, h->fu_unit[0] && h->fu_unit[1], h->dd, hw,
-                                              h->stream)) {
+                                              h->stream, true)) {
+            h->qd_now = h->dp.qdown != nullptr && h->dp.nqd > 0;
             if (e_mid) HIP_TRY(hipEventRecord(e_mid, h->stream));
             launch_riv(h, y, dy, false);             // after the boundary workgroups, which saw the halo
             // optional join of the comm stream (normally complete long before: the boundary workgroups saw its flag),

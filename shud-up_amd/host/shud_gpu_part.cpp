@@ -107,16 +107,34 @@ std::vector<double> test_state(const double *y0, int64_t ny, int ne, int k) {
     return y;
 }
 
-// the RCCL id file of one job: "<token>\n" + 128 id bytes.  The token names the job: torchrun's run id, the
-// rendezvous address and the launcher's pid (every local rank of one job is a child of the same launcher process —
-// torchrun's agent or bench.py — and a later job's launcher is another process; static rendezvous leaves the run id
-// at "none", so address and port alone would accept an earlier job's file).  SHUD_JOB_ID, when set by the caller,
-// replaces the launcher pid.
+// the RCCL id file of one job: "<token>\n" + 128 id bytes.  The token names the job, from the most specific source
+// the environment offers: SHUD_JOB_ID when the caller sets it (any launcher, several nodes sharing the outdir, per-rank
+// wrapper scripts); else torchrun's run id when it is a real one (static rendezvous leaves it at "none"), with the
+// rendezvous address and port; else that address and port with the launcher's pid (every local rank of one job is a
+// direct child of the same launcher process — torchrun's agent or bench.py — and a later job's launcher is another
+// process; address and port alone would accept an earlier job's file).  The last form needs single-node ranks that
+// are direct children of one launcher: a rank that finds a fresh id file under another token says so and stops.
 std::string job_token() {
     const char *run = getenv("TORCHELASTIC_RUN_ID"), *ma = getenv("MASTER_ADDR"), *mp = getenv("MASTER_PORT");
     const char *jid = getenv("SHUD_JOB_ID");
-    const std::string who = jid ? std::string(jid) : "ppid" + std::to_string((long)getppid());
-    return std::string(run ? run : "-") + ":" + (ma ? ma : "-") + ":" + (mp ? mp : "-") + ":" + who;
+    if (jid && *jid) return std::string("job:") + jid;
+    const std::string addr = std::string(ma ? ma : "-") + ":" + (mp ? mp : "-");
+    if (run && *run && strcmp(run, "none") != 0) return std::string("run:") + run + ":" + addr;
+    return "ppid:" + addr + ":" + std::to_string((long)getppid());
+}
+
+// the token of a fresh id file (written after `not_before`), "" if there is none
+std::string id_file_token(const std::string &f, time_t not_before) {
+    struct stat st;
+    if (stat(f.c_str(), &st) != 0 || st.st_mtime < not_before) return "";
+    FILE *fp = fopen(f.c_str(), "rb");
+    if (!fp) return "";
+    char buf[512];
+    const size_t n = fread(buf, 1, sizeof buf - 1, fp);
+    fclose(fp);
+    buf[n] = 0;
+    const char *nl = strchr(buf, '\n');
+    return nl ? std::string(buf, nl - buf) : "";
 }
 
 // the 128 id bytes of `f` if it carries `token` and was written after `not_before` (seconds since the epoch)
@@ -311,7 +329,16 @@ int shud_gpu_rhs_partition(shud_project_t p, int nparts_check, bool bench, int n
                 nccl_id = read_id_file(idf, token, not_before);
                 if (nccl_id.empty()) std::this_thread::sleep_for(std::chrono::milliseconds(100));
             }
-            if (nccl_id.empty()) { fprintf(stderr, "rank %d: no RCCL id in %s\n", rank, idf.c_str()); return 1; }
+            if (nccl_id.empty()) {
+                const std::string other = id_file_token(idf, not_before);
+                if (!other.empty() && other != token)
+                    fprintf(stderr, "rank %d: %s holds the RCCL id of job '%s', not this job '%s' (ranks of one job "
+                                    "must share SHUD_JOB_ID, or be direct children of one launcher on one node)\n",
+                            rank, idf.c_str(), other.c_str(), token.c_str());
+                else
+                    fprintf(stderr, "rank %d: no RCCL id in %s\n", rank, idf.c_str());
+                return 1;
+            }
         }
         if (shud_plan_build(&mesh, ele_part.data(), K, rank, &q.plan) || shud_plan_partition(q.plan, &q.part) ||
             shud_plan_local_mesh(q.plan, &mesh, &par, &q.lmesh, &q.lpar))

@@ -43,3 +43,28 @@ def test_single_gpu_does_not_spawn():
     assert r.returncode == 0
     d = json.loads(r.stdout.strip())
     assert d["world_size"] == 1 and d["rank"] == 0
+
+
+def test_hung_rank_is_named_by_its_own_watchdog():
+    """A rank that never leaves a phase: its in-rank watchdog (faulthandler, armed per phase at N > 1) exits it after
+    the phase's bound (scaled down here), the launcher stops the others and names the rank and the phase."""
+    import time
+    t0 = time.monotonic()
+    r = _run(["--gpus", "3", "--dry-launch"], {"SHUD_BENCH_DRY_HANG_RANK": "1", "SHUD_BENCH_PHASE_SCALE": "0.05"})
+    el = time.monotonic() - t0
+    assert r.returncode != 0, r.stderr
+    assert "rank 1 exited with status 1 in phase 'dry_hang'" in r.stderr, r.stderr[-2000:]
+    assert el < 60, el
+
+
+def test_hung_rank_is_stopped_by_the_launcher():
+    """The same hang with the in-rank watchdog off: the launcher's own watchdog (bound + grace) terminates every
+    rank, exits 124 and names the stuck rank and phase."""
+    import time
+    t0 = time.monotonic()
+    r = _run(["--gpus", "2", "--dry-launch"], {"SHUD_BENCH_DRY_HANG_RANK": "1", "SHUD_BENCH_PHASE_SCALE": "0.05",
+                                                "SHUD_BENCH_RANK_WATCHDOG": "0", "SHUD_BENCH_GRACE_S": "2"})
+    el = time.monotonic() - t0
+    assert r.returncode == 124, (r.returncode, r.stderr[-2000:])
+    assert "watchdog: rank 1 stuck in phase 'dry_hang'" in r.stderr, r.stderr[-2000:]
+    assert el < 60, el

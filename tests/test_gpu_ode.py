@@ -110,6 +110,29 @@ def test_device_stop_time_one_step_dky(kat, device_order):
     kat.shud_kat_ode_free(u)
 
 
+def test_state_device_complete_for_other_streams(kat, device_order):
+    """shud_ode_state_device after lazy one-step solves (no y_out: zn[0]'s completion still deferred on the
+    integrator's non-blocking stream): the pointer it returns is read at once by a plain hipMemcpy on the null
+    stream and must hold y(tcur) bit for bit (the call now completes and synchronizes)."""
+    n = 7 * 40000
+    u, fn = _dev(kat, "decayn", n)
+    y0 = 1.0 + 0.5 * np.sin(np.arange(n))
+    d = rt.OdeSolver(None, 0.0, y0, 1e-6, 1e-10, 1e-5, 0.0, 0.0, fn=fn)
+    o = oracle.OracleOde("decayn", 0.0, y0, 1e-6, 1e-10, 1e-5, 0.0, 0.0)
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    for k in range(6):
+        d.solve(1.0, one_step=True, y_out=False)
+        fo, to, yo = o.solve(1.0, one_step=True)
+        ptr = d.state_device()
+        assert ptr
+        got = np.empty(n)
+        assert hip.hipMemcpy(got.ctypes.data, ptr, 8 * n, 2) == 0          # hipMemcpyDeviceToHost, null stream
+        assert np.array_equal(got, yo), (k, np.abs(got - yo).max())
+    d.close()
+    kat.shud_kat_ode_free(u)
+
+
 def _close_traj(yd, yo, what, frac=1e-6, rtol=1e-4, atol=1e-4):
     """per-state error below `frac` of the solver's own error weight 1/ewt = rtol|y| + atol"""
     err = np.abs(yd - yo)

@@ -90,6 +90,61 @@ def test_river_junctions(mode, oracle_mod, layout):
     _compare_sequence(m, cases.states(m, None, 2, seed=21), mode, oracle_mod, label="junctions", layout=layout)
 
 
+def _junction_model():
+    from shud_rhs import synth
+    m = synth.synth_model(20000)
+    down = m.riv_down.astype(np.int64)
+    nup = np.bincount(down[down >= 0], minlength=m.num_riv)
+    heads = np.nonzero(nup == 0)[0]
+    t_big = int(np.nonzero((nup == 0) & (down >= 0))[0][0])
+    t_three = int(np.nonzero(nup == 1)[0][0])
+    movers = [h for h in heads if h not in (t_big, t_three)]
+    down[movers[:14]] = t_big
+    down[movers[14:16]] = t_three
+    m.riv_down = down.astype(np.int32)
+    return m, None
+
+
+@pytest.mark.parametrize("mode", [abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP])
+def test_river_paths_bit_identical(mode, oracle_mod, monkeypatch):
+    """The river kernel's build paths give the same bits: QrivDown from the element launch's pre-pass slots
+    (default) or recomputed from the reach records (SHUD_RHS_QD=0), with 6 or 8 segments per gather batch
+    (SHUD_RIV_SB; the handle otherwise picks one from the mesh).  ccw, heihe, the branch variant and the junction
+    shapes, 3 stateful calls on 2 states, every river diagnostic; one path also against the oracle."""
+    rt = _runtime()
+    for label, (m, y0) in (("ccw", cases.ccw()), ("heihe", cases.heihe()), ("variant", cases.variant()),
+                           ("junctions", _junction_model())):
+        ys = cases.states(m, y0, 2, seed=5)
+        outs = {}
+        for qd in ("1", "0"):
+            for sb in ("6", "8"):
+                monkeypatch.setenv("SHUD_RHS_QD", qd)
+                monkeypatch.setenv("SHUD_RIV_SB", sb)
+                g = rt.RhsHandle(m, mode=mode)
+                assert g.layout()["packed"]
+                g.set_step_inputs()
+                seq = [g.eval(0.0, y) for y in ys for _ in range(3)]
+                dg = g.diagnostics()
+                outs[(qd, sb)] = (seq, {k: dg[k] for k in ("qriv_down", "qriv_up", "qriv_surf", "qriv_sub")})
+                g.close()
+        ref_seq, ref_dg = outs[("0", "8")]
+        for key, (seq, dg) in outs.items():
+            for c, (a, b) in enumerate(zip(seq, ref_seq)):
+                assert np.array_equal(a, b, equal_nan=True), f"{label} QD={key[0]} SB={key[1]} call {c}"
+            for k in dg:
+                assert np.array_equal(dg[k], ref_dg[k], equal_nan=True), f"{label} QD={key[0]} SB={key[1]} {k}"
+        o = oracle_mod.OracleRhs(m, mode)
+        o.set_step_inputs()
+        seq = outs[("1", "6")][0]
+        k = 0
+        for si, y in enumerate(ys):
+            for c in range(3):
+                assert_close(seq[k], o.eval(0.0, y)[0], what=f"{label} QD SB6 state {si} call {c}")
+                k += 1
+    monkeypatch.delenv("SHUD_RHS_QD")
+    monkeypatch.delenv("SHUD_RIV_SB")
+
+
 @pytest.mark.parametrize("mode", [abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP])
 def test_variant_branches(mode, oracle_mod, layout):
     m, y = cases.variant()

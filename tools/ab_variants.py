@@ -7,6 +7,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 import ctypes as C
 
@@ -43,6 +44,11 @@ def lib_for(v):
 
 
 def env_for(v):
+    # pk+NAME=VAL[+NAME=VAL]: the packed kernel with extra environment (run-time switches, e.g. pk+SHUD_RHS_QD=0)
+    if v.startswith("pk+"):
+        e = {"SHUD_RHS_PACKED": "1", "SHUD_RHS_ELE_VARIANT": "0", "SHUD_RHS_SEG_ORDER": "element"}
+        e.update(kv.split("=", 1) for kv in v[3:].split("+"))
+        return e
     if v.startswith("lib:"):
         return {"SHUD_RHS_PACKED": "1", "SHUD_RHS_ELE_VARIANT": "0", "SHUD_RHS_SEG_ORDER": "element"}
     if v.startswith("soa"):
@@ -51,11 +57,17 @@ def env_for(v):
             "SHUD_RHS_SEG_ORDER": "reach" if v == "pkR" else "element"}
 res = {v: [] for v in vs}
 rres = {v: [] for v in vs}
+wres = {v: [] for v in vs}
+_saved = {}
 ref = None
 _libs["prod"] = runtime.lib()
 for rnd in range(a.rounds):
     for v in vs:
-        os.environ.update(env_for(v))
+        for k in _saved:                           # undo the previous variant's extra switches
+            os.environ.pop(k, None)
+        ev = env_for(v)
+        _saved = {k: 1 for k in ev}
+        os.environ.update(ev)
         runtime._LIB = lib_for(v)                 # every call of this handle goes to the variant's library
         h = runtime.RhsHandle(m)
         h.set_step_inputs()
@@ -69,9 +81,17 @@ for rnd in range(a.rounds):
         ms, per = h.time_kernels(0.0, dp, dd, a.reps)
         res[v].append(per["shud_ele_kernel"])
         rres[v].append(per["shud_riv_kernel"])
+        # event-free: reps back-to-back evals between two synchronizes (what a caller's RHS loop sees)
+        h.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.reps):
+            h.eval_device(0.0, dp, dd)
+        h.synchronize()
+        wres[v].append((time.perf_counter() - t0) / a.reps * 1e3)
         print(f"round {rnd} variant {v:5s} {h.layout()}: ele {per['shud_ele_kernel']:.4f} ms riv {per['shud_riv_kernel']:.4f} "
-              f"ms  bit-identical={same}", flush=True)
+              f"ms  wall {wres[v][-1]:.4f} ms/eval  bit-identical={same}", flush=True)
         h.device_free(dp); h.device_free(dd); h.close()
         runtime._LIB = _libs["prod"]
 print(json.dumps({"num_ele": m.num_ele, "ele_ms_median": {v: float(np.median(t)) for v, t in res.items()},
-                  "riv_ms_median": {v: float(np.median(t)) for v, t in rres.items()}}))
+                  "riv_ms_median": {v: float(np.median(t)) for v, t in rres.items()},
+                  "wall_ms_per_eval_median": {v: float(np.median(t)) for v, t in wres.items()}}))
