@@ -105,6 +105,17 @@ constexpr int CF_LDS_STRIDE = CF_STRIDE;   // the HBM table's record layout, cop
 #ifndef SHUD_ELE_WAVES
 #define SHUD_ELE_WAVES 5        // min waves per SIMD: <= 96 VGPRs (rolled edge loop, no spills)
 #endif
+// elements per workgroup of the single-launch kernel (A/B: 512 / 1024 copy the LDS class table fewer times)
+#ifndef SHUD_ELE_BS
+#define SHUD_ELE_BS 256
+#endif
+constexpr int kEleBS = SHUD_ELE_BS;
+// SHUD_EABL (timing-only ablation builds for the per-phase attribution, results are WRONG when != 0): bit 0 the
+// segment loop, 1 the neighbour eff_kh (KsatH instead), 2 the edge loop, 3 f_etFlux, 4 satKfun (satkr = satn),
+// 5 the report_w ballots, 6 infiltration + recharge
+#ifndef SHUD_EABL
+#define SHUD_EABL 0
+#endif
 // One 256-element tile per workgroup.  (Persistent workgroups — one per resident slot looping over XCD-chunked
 // tiles, the class table copied to LDS once per workgroup — measured 0.735 vs 0.657 ms: the tile loop took the
 // kernel to 96 VGPRs with spills, profiles/r03/ab_persist/.)
@@ -185,26 +196,26 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
                                          const OwnRec &own);
 
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
-__global__ void __launch_bounds__(256, SHUD_ELE_WAVES)
+__global__ void __launch_bounds__(kEleBS, SHUD_ELE_WAVES)
 shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int i0, int n_compute, int cur,
                        DevDiag dg, DevLake lk, int per8, int nb_e, int nb_q) {
     extern __shared__ double lct[];                       // ncls * CF_LDS_STRIDE doubles when LCT
     if (nb_q) {
         const int qb = qd_block(nb_e, nb_q);
         if (qb >= 0) {
-            const int r = qb * 256 + (int)threadIdx.x;
+            const int r = qb * kEleBS + (int)threadIdx.x;
             if (r < p.nqd) qd_pre<MODE>(m, p, Y, r);
             return;
         }
     }
-    const int i = i0 + tile_of(per8, ele_block(nb_q)) * 256 + (int)threadIdx.x;   // elements [i0, n_compute)
+    const int i = i0 + tile_of(per8, ele_block(nb_q)) * kEleBS + (int)threadIdx.x;   // elements [i0, n_compute)
     const bool act = i < n_compute;
     double tv[kTabBatch];
-    if (LCT) tab_issue<256>(p, tv);
+    if (LCT) tab_issue<kEleBS>(p, tv);
     OwnRec own;
     if (act) own = load_own<FU1, GH>(p, Y, i, cur);
     if (LCT) {
-        tab_store<256>(p, tv, lct);
+        tab_store<kEleBS>(p, tv, lct);
         __syncthreads();
     }
     if (act) ele_body<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH>(m, p, Y, dy, i, cur, dg, lk, lct, own);
@@ -346,7 +357,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
         ekh = CL(KsatH); deficit = 0.; satn = 1.; theta = CL(ThetaS); satkr = 1.0;
     } else {
         ekh = eff_kh(ugw, aq, CL(macD), CL(macKsatH), CL(vAreaF), CL(KsatH));
-        report_w(m.err, ekh < 0. || ekh > 1e9, 0x02u, 1, i);
+        if (!(SHUD_EABL & 32)) report_w(m.err, ekh < 0. || ekh > 1e9, 0x02u, 1, i);
         deficit = aq - ugw;
         const double ThS = CL(ThetaS), ThR = CL(ThetaR);
         if (deficit <= 0.) { deficit = 0.; satn = 1.; theta = ThS; }
@@ -354,7 +365,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
         if (satn > 0.99) { satn = 1.0; satkr = 1.0; theta = ThS; }
         else if (satn <= K_ZERO) { satn = 0.; satkr = 0.; theta = ThR; }
         else {   // satKfun, Equations.cpp:136-141
-            satkr = sat_kfun(satn, CL(ex1), CL(ex2));                    // n/(n-1), (n-1)/n
+            satkr = (SHUD_EABL & 16) ? satn : sat_kfun(satn, CL(ex1), CL(ex2));   // n/(n-1), (n-1)/n
         }
     }
 
@@ -372,7 +383,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
         eic = 0.;                                 // fun_Ele_lakeVertical: qEleE_IC = 0 (carried)
         if (DIAG) { dg.q_es[i] = 0.; dg.q_eu[i] = 0.; dg.q_eg[i] = 0.; dg.q_tu[i] = 0.; dg.q_tg[i] = 0.;
                     dg.q_eta[i] = 0. + snp.y + 0.; }
-    } else if (MODE == 0) {
+    } else if (MODE == 0 && !(SHUD_EABL & 8)) {
         const double satn_prev = csv.x;
         const double va = CL(VegFrac), vb = CL(vb), pj = CL(pj);
         const double pet = snp.y, ptr = stl.x;
@@ -388,13 +399,15 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
             else { Tg = 0.; Tu = rmin(rmax(0., uus), ibeta * (ptr - eic)) * pj * va; }
         } else { Tg = Tu = eic = 0.; }
         const double trans = Tg + Tu, evapo = Eu + Eg + Es, eta = eic + evapo + trans;
-        report_w(m.err, eta > etp * 2., 0x10u, 4, i, true);      // printf warning, MD_ET.cpp:391-393
+        if (!(SHUD_EABL & 32)) report_w(m.err, eta > etp * 2., 0x10u, 4, i, true);   // printf warning, MD_ET.cpp:391-393
         // CheckNonNegative (functions.cpp:148-154): x < 0 || isnan || isinf || |x - NA| < ZERO is exactly
         // "NaN, an infinity, or a negative normal/subnormal" (-0.0 passes; x ~ -9999 is negative): one
         // v_cmp_class per value
         const bool neg = bad_nonneg(Es) || bad_nonneg(Eu) || bad_nonneg(Eg) || bad_nonneg(Tu) || bad_nonneg(Tg);
-        report_w(m.err, neg, 0x04u, 2, i);
-        report_w(m.err, !neg && (nan_or_inf(eta) || nan_or_inf(evapo) || nan_or_inf(trans)), 0x08u, 3, i);
+        if (!(SHUD_EABL & 32)) {
+            report_w(m.err, neg, 0x04u, 2, i);
+            report_w(m.err, !neg && (nan_or_inf(eta) || nan_or_inf(evapo) || nan_or_inf(trans)), 0x08u, 3, i);
+        }
         if (DIAG) { dg.q_es[i] = Es; dg.q_eu[i] = Eu; dg.q_eg[i] = Eg; dg.q_tu[i] = Tu; dg.q_tg[i] = Tg;
                     dg.q_eta[i] = eta; dg.i_beta[i] = ibeta; }
     }
@@ -402,7 +415,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
 
     // ---- Flux_Infiltration (Element.cpp:271-303) and Flux_Recharge (:304-335); zero on lake elements ----
     double qi = 0., qex = 0., qr = 0.;
-    if (!is_lake) {
+    if (!is_lake && !(SHUD_EABL & 64)) {
         const double kmax = CL(kmax);
         const double av = usf + snp.x;
         if (ugw + uus > aq || deficit < uus) {
@@ -441,7 +454,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     // ---- own river segments (fun_Seg_surface / fun_Seg_sub) and Qe2r (PassValue) ----
     const double dep = CL(depression), rgh = CL(rough);
     double qe2r_surf = 0., qe2r_sub = 0.;
-    if (nseg) {
+    if (nseg && !(SHUD_EABL & 1)) {
         const double isf_seg = rmax(0., usf - q_infil + q_exfil);
         for (int k = sfirst, k1 = k + nseg; k < k1; k++) {
             // one 48-B element-sorted record per segment: its own fields plus its reach's statics
@@ -495,7 +508,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     const double area = ldnt(at(p.area, o8));          // in flight across the edge loop
 #endif
 #pragma unroll 1
-    for (int j = 0; j < (is_lake ? 0 : 3); j++) {     // lake elements: fun_Ele_lakeHorizon, all zero
+    for (int j = 0; j < ((is_lake || (SHUD_EABL & 4)) ? 0 : 3); j++) {   // lake elements: fun_Ele_lakeHorizon, all zero
         const int nb = j == 0 ? mt.x : j == 1 ? mt.y : mt.z;
         const int nc = nb >= 0 ? nb : i;                  // boundary edge: harmless in-bounds loads
         // (edge 0's loads issued right after the own record instead — held through the vertical physics — took
@@ -556,7 +569,8 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
             if (dhg > 0. && ugw <= 0.02) q = 0.;
             else if (dhg < 0. && ugn <= 0.02) q = 0.;
             else {
-                const double ekn = eff_kh(ugn, zsn - zbn, CN(macD), CN(macKsatH), CN(vAreaF), CN(KsatH));
+                const double ekn = (SHUD_EABL & 2) ? CN(KsatH)
+                                                   : eff_kh(ugn, zsn - zbn, CN(macD), CN(macKsatH), CN(vAreaF), CN(KsatH));
                 const double ymg = (rmax(ugw, 0.) + rmax(ugn, 0.)) * .5;
                 const double grad = D2N_DIV(dhg);
                 const double kmean = 0.5 * (ekh + ekn);
@@ -587,7 +601,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     }
     if (DIAG && is_lake)
         for (int j = 0; j < 3; j++) { dg.qele_surf[j * NEl + i] = 0.; dg.qele_sub[j * NEl + i] = 0.; }
-    if (MODE == 0) report_w(m.err, nan_q, 0x01u, 0, i);       // CheckNANij, MD_f.cpp:73-74
+    if (MODE == 0 && !(SHUD_EABL & 32)) report_w(m.err, nan_q, 0x01u, 0, i);   // CheckNANij, MD_f.cpp:73-74
 
     // ---- f_applyDY element part (MD_f.cpp:88-150 / MD_f_omp.cpp:26-46) ----
 #if !SHUD_AREA_EARLY
@@ -940,11 +954,11 @@ static void launch_big(const DevMesh &m, const DevPacked &p, const YView &Y, dou
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
 static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1, int cur,
                      const DevDiag &dg, const DevLake &lk, hipStream_t s, int nq = 0) {
-    int nb = (i1 - i0 + 255) / 256;
+    int nb = (i1 - i0 + kEleBS - 1) / kEleBS;
     nb = (nb + 7) / 8 * 8;                  // block_id<1> deals blocks to XCDs in contiguous chunks
-    const int nbq = nq > 0 ? ((nq + 255) / 256 + 7) / 8 * 8 : 0;
+    const int nbq = nq > 0 ? ((nq + kEleBS - 1) / kEleBS + 7) / 8 * 8 : 0;
     const size_t lds = LCT ? (size_t)p.ncls * CF_LDS_STRIDE * sizeof(double) : 0;
-    hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH>), dim3(nb + nbq), dim3(256), lds, s,
+    hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH>), dim3(nb + nbq), dim3(kEleBS), lds, s,
                        m, p, Y, dy, i0, i1, cur, dg, lk, nb / 8, nb, nbq);
 }
 
