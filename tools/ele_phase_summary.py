@@ -17,7 +17,7 @@ DESC = {"prod": "production", "e1": "segment loop", "e2": "neighbour eff_kh (Ksa
 cnt = {}
 for n in names:
     agg = collections.defaultdict(list)
-    for f in glob.glob(f"{d}/sq_{n}/**/*counter_collection.csv", recursive=True):
+    for f in glob.glob(f"{d}/sq_{n}/**/*counter_collection.csv", recursive=True) + glob.glob(f"{d}/sq_{n}_counters.csv"):
         for r in csv.DictReader(open(f)):
             if "ele_kernel" in r["Kernel_Name"]:
                 agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
