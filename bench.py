@@ -682,7 +682,7 @@ def kernel_src_hash():
     csrc = os.path.join(ROOT, "shud-up_amd", "csrc")
     for f in sorted(os.listdir(csrc)):
         if f.startswith(("shud_ele_packed", "shud_kernels", "shud_dev", "shud_physics", "shud_rhs.cpp",
-                         "shud_handle")):
+                         "shud_handle", "shud_pow")):
             with open(os.path.join(csrc, f), "rb") as fh:
                 hh.update(f.encode() + b"\0" + fh.read())
     with open(os.path.join(ROOT, "shud-up_amd", "Makefile"), "rb") as fh:

@@ -40,12 +40,13 @@ __global__ void kat_kernel(int fn, int k, const double *__restrict__ in, int n, 
     out[t] = r;
 }
 
-// pow_pos (shud_physics.h) next to OCML's full pow on the same (x, y) pairs: which = 0 pow, 1 pow_pos
+// pow_pos / pow_tab (shud_physics.h, shud_powtab.h) next to OCML's full pow on the same (x, y) pairs: which = 0 pow,
+// 1 pow_pos, 2 pow_tab
 __global__ void kat_pow_kernel(int which, const double *__restrict__ xy, int n, double *__restrict__ out) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
     const double x = xy[2 * t], y = xy[2 * t + 1];
-    out[t] = which ? pow_pos(x, y) : pow(x, y);
+    out[t] = which == 2 ? shud_pow_tab(x, y) : which ? pow_pos(x, y) : pow(x, y);
 }
 extern "C" int shud_kat_pow(int which, const double *h_xy, int n, double *h_out) {
     if (n <= 0) return -1;

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "shud_dev.h"
+#include "shud_powtab.h"
 
 // SHUD_ABL (timing-only ablation builds, never shipped): bit 0 pow, 1 cos, 2 cbrt, 3 division, 4 sqrt are
 // replaced by a single cheap op so their share of the element kernel's time can be measured.
@@ -217,7 +218,17 @@ __device__ __forceinline__ double pow_pos(double x, double y) {
 #ifndef SHUD_POWPOS
 #define SHUD_POWPOS 1
 #endif
-#if SHUD_POWPOS && !(SHUD_ABL & 1)
+// satKfun's pow: shud_pow_tab (shud_powtab.h, default: table-driven log/exp, ~60 VALU, within 0.66 ulp of x^y and
+// equal to glibc's pow on 99.9 % of satKfun's domain — tests/test_kat.py); SHUD_POWTAB=0: pow_pos (OCML's pow core,
+// ~180 VALU, the device pow's bits)
+#ifndef SHUD_POWTAB
+#define SHUD_POWTAB 1
+#endif
+#if SHUD_ABL & 1
+#define SPOW_SAT(a, b) SPOW(a, b)
+#elif SHUD_POWTAB
+#define SPOW_SAT(a, b) shud_pow_tab(a, b)
+#elif SHUD_POWPOS
 #define SPOW_SAT(a, b) pow_pos(a, b)
 #else
 #define SPOW_SAT(a, b) SPOW(a, b)
