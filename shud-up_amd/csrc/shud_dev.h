@@ -82,13 +82,17 @@ inline bool cdiv_divisor_ok(double b) {
 #define SHUD_LDS_CLS_MAX 128
 #endif
 constexpr int kLdsClassMax = SHUD_LDS_CLS_MAX;
-// most classes a 1024-thread workgroup stages in LDS (600 x 33 x 8 B = 155 KiB of the CU's 160 KiB: one workgroup
-// per CU, 4 waves/SIMD) — models with 129..600 distinct parameter tuples
-constexpr int kLdsClassMaxBig = 600;
+// pow_tab's log + exp tables (shud_pow_tab.h: 256 x 4 + 128 x 2 doubles), staged in LDS after the class table
+constexpr int kPowTabDoubles = 4 * 256 + 2 * 128;
+// most classes a 1024-thread workgroup stages in LDS ((560 x 33 + 1280) x 8 B = 154 KiB of the CU's 160 KiB: one
+// workgroup per CU, 4 waves/SIMD) — models with 129..560 distinct parameter tuples
+constexpr int kLdsClassMaxBig = 560;
 
 struct DevPacked {
-    const double *ctab;     // [ncls][CF_STRIDE] record-major: one class's fields share 2-3 cache lines
+    const double *ctab;     // [ncls][CF_STRIDE] record-major: one class's fields share 2-3 cache lines; then, from
+                            //   double pt_off (even: 16-B aligned), pow_tab's log and exp tables (kPowTabDoubles)
     int ncls;
+    int pt_off, ntab;       // ntab = pt_off + kPowTabDoubles: the doubles a workgroup copies into LDS
     const double2 *zz;      // {z_surf, z_bottom}  (aquifer_depth == z_surf - z_bottom, checked at create)
     const int4 *meta;       // {nabr0, nabr1, nabr2, cf}: cf bits 0-7 iBC (int8), 8-9 iSS class,
                             //   10-15 #river segments, 16-30 class id, 31 lake element

@@ -116,6 +116,11 @@ constexpr int kEleBS = SHUD_ELE_BS;
 #ifndef SHUD_EABL
 #define SHUD_EABL 0
 #endif
+// pow_tab's tables read from the workgroup's LDS copy (default) or gathered from the class-table buffer in HBM/L2
+// (SHUD_PT_LDS=0, A/B)
+#ifndef SHUD_PT_LDS
+#define SHUD_PT_LDS 1
+#endif
 // One 256-element tile per workgroup.  (Persistent workgroups — one per resident slot looping over XCD-chunked
 // tiles, the class table copied to LDS once per workgroup — measured 0.735 vs 0.657 ms: the tile loop took the
 // kernel to 96 VGPRs with spills, profiles/r03/ab_persist/.)
@@ -150,7 +155,7 @@ __device__ __forceinline__ OwnRec load_own(const DevPacked &p, const YView &Y, i
 constexpr int kTabBatch = 8;
 template <int BS>
 __device__ __forceinline__ void tab_issue(const DevPacked &p, double (&tv)[kTabBatch]) {
-    const int nt = p.ncls * CF_LDS_STRIDE;
+    const int nt = p.ntab;
 #pragma unroll
     for (int k = 0; k < kTabBatch; k++) {
         const int t = (int)threadIdx.x + k * BS;
@@ -159,7 +164,7 @@ __device__ __forceinline__ void tab_issue(const DevPacked &p, double (&tv)[kTabB
 }
 template <int BS>
 __device__ __forceinline__ void tab_store(const DevPacked &p, const double (&tv)[kTabBatch], double *lct) {
-    const int nt = p.ncls * CF_LDS_STRIDE;
+    const int nt = p.ntab;
 #pragma unroll
     for (int k = 0; k < kTabBatch; k++) {
         const int t = (int)threadIdx.x + k * BS;
@@ -365,7 +370,9 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
         if (satn > 0.99) { satn = 1.0; satkr = 1.0; theta = ThS; }
         else if (satn <= K_ZERO) { satn = 0.; satkr = 0.; theta = ThR; }
         else {   // satKfun, Equations.cpp:136-141
-            satkr = (SHUD_EABL & 16) ? satn : sat_kfun(satn, CL(ex1), CL(ex2));   // n/(n-1), (n-1)/n
+            // n/(n-1), (n-1)/n; pow_tab's tables from the workgroup's LDS copy (or the L2 class table's buffer)
+            const double *pt = (LCT && SHUD_PT_LDS ? lct : p.ctab) + p.pt_off;
+            satkr = (SHUD_EABL & 16) ? satn : sat_kfun(satn, CL(ex1), CL(ex2), pt, pt + 4 * SHUD_PT_LOG_N);
         }
     }
 
@@ -940,12 +947,12 @@ static void launch_big(const DevMesh &m, const DevPacked &p, const YView &Y, dou
                        const DevDiag &dg, const DevLake &lk, hipStream_t s) {
     int nb = (i1 - i0 + 1023) / 1024;
     nb = (nb + 7) / 8 * 8;                  // block_id<1> deals blocks to XCDs in contiguous chunks
-    const size_t lds = (size_t)p.ncls * CF_LDS_STRIDE * sizeof(double);
+    const size_t lds = (size_t)p.ntab * sizeof(double);
     auto *fn = shud_ele_kernel_packed_big<MODE, OPEN, DIAG, FU1, GH>;
     static bool attr = false;               // dynamic LDS above 64 KiB must be allowed per kernel
     if (!attr) {
         (void)hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)(kLdsClassMaxBig * CF_LDS_STRIDE * sizeof(double)));
+                                  (int)((kLdsClassMaxBig * CF_LDS_STRIDE + 1 + kPowTabDoubles) * sizeof(double)));
         attr = true;
     }
     hipLaunchKernelGGL(fn, dim3(nb), dim3(1024), lds, s, m, p, Y, dy, i0, i1, cur, dg, lk, nb / 8);
@@ -957,7 +964,7 @@ static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, doubl
     int nb = (i1 - i0 + kEleBS - 1) / kEleBS;
     nb = (nb + 7) / 8 * 8;                  // block_id<1> deals blocks to XCDs in contiguous chunks
     const int nbq = nq > 0 ? ((nq + kEleBS - 1) / kEleBS + 7) / 8 * 8 : 0;
-    const size_t lds = LCT ? (size_t)p.ncls * CF_LDS_STRIDE * sizeof(double) : 0;
+    const size_t lds = LCT ? (size_t)p.ntab * sizeof(double) : 0;
     hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH>), dim3(nb + nbq), dim3(kEleBS), lds, s,
                        m, p, Y, dy, i0, i1, cur, dg, lk, nb / 8, nb, nbq);
 }
@@ -1006,7 +1013,7 @@ bool launch_element_kernel_packed_fold(const DevMesh &m, const DevPacked &p, con
     if (n_int <= 0 || n_all <= n_int || p.ncls > LDS_CLS_MAX) return false;
     const int nb_int = ((n_int + 255) / 256 + 7) / 8 * 8, nb_b = (n_all - n_int + 255) / 256;
     const int nbq = (with_qd && p.qdown && p.nqd > 0) ? (p.nqd + 255) / 256 : 0;
-    const size_t lds = (size_t)p.ncls * CF_LDS_STRIDE * sizeof(double);
+    const size_t lds = (size_t)p.ntab * sizeof(double);
 #define LF(MO, OP, FU) hipLaunchKernelGGL((shud_ele_kernel_packed_fold<MO, OP, FU>), dim3(nb_int + nb_b + nbq), dim3(256), \
                                           lds, s, m, p, Y, dy, n_int, n_all, cur, dg, nb_int / 8, nb_int, hw,          \
                                           nb_int + nb_b)

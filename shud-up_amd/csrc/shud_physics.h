@@ -236,10 +236,19 @@ __device__ __forceinline__ double pow_pos(double x, double y) {
 
 // satKfun, Equations.cpp:136-141, with the class exponents ex1 = n/(n-1), ex2 = (n-1)/n precomputed.
 // Both bases are positive here: satn in (ZERO, 0.99] (the callers' clamps), 1 - satn^ex1 in (0, 1];
-// exponents are class constants of Beta > 1 (checked by the handle) -> pow_pos
-__device__ __forceinline__ double sat_kfun(double satn, double ex1, double ex2) {
+// exponents are class constants of Beta > 1 (checked by the handle).  lt / et: pow_tab's log / exp tables (the element
+// kernel passes its LDS copy; default: __constant__ memory)
+__device__ __forceinline__ double sat_kfun(double satn, double ex1, double ex2, const double *lt, const double *et) {
+#if SHUD_POWTAB && !(SHUD_ABL & 1)
+    const double tmp = -1. + shud_pow_tab_t(1. - shud_pow_tab_t(satn, ex1, lt, et), ex2, lt, et);
+#else
+    (void)lt; (void)et;
     const double tmp = -1. + SPOW_SAT(1. - SPOW_SAT(satn, ex1), ex2);
+#endif
     return SSQRT(satn) * tmp * tmp;
+}
+__device__ __forceinline__ double sat_kfun(double satn, double ex1, double ex2) {
+    return sat_kfun(satn, ex1, ex2, shud_pt_logtab, shud_pt_exptab);
 }
 // SoilMoistureStress, is_sm_et.cpp:131-140 (truncated PI), with dth = ThetaS - ThetaR and
 // fcmr = ThetaS * 0.75 - ThetaR; b = (SatRatio * dth - ThetaR) / fcmr

@@ -6,9 +6,11 @@
 // Why: OCML's pow core (pow_pos) costs ~180 VALU per call — an extended-precision log built from ~60 dependent
 // two-sum steps and an extended exp — and satKfun's two calls were 314 of the element kernel's 1,409 VALU per wave
 // (profiles/r05/ele_attr).  Here the log is a 256-entry table + a degree-8 polynomial in double-double and the exp a
-// 128-entry table of 2^(i/128) + a degree-5 polynomial: ~60 VALU and 5 table loads per call, error within ~0.52 ulp
+// 128-entry table of 2^(i/128) + a degree-5 polynomial: ~60 VALU and 3 table loads per call, error within ~0.51 ulp
 // of the true x^y (tests/test_kat.py measures it), where glibc's pow (the reference's) is within ~0.52 ulp too and
-// OCML's within ~1 ulp.
+// OCML's within ~1 ulp.  The element kernel reads the tables from its LDS copy (the per-lane gathers from
+// __constant__ memory measured 4 % slower than OCML's pow core: 10 divergent vector loads per element,
+// profiles/r05/powtab/).
 //
 // log x = k ln2 + log c + log1p(z/c - 1) with x = 2^k z, z in [OFF, 2 OFF), invc = 1/c to 9 significant bits so
 // r = z*invc - 1 is exact in one fma; exp(t) = 2^(j/128) 2^(k') exp(r) with r = t - (128 k' + j) ln2/128.
@@ -29,16 +31,31 @@
 
 SHUD_PT_FN uint64_t shud_pt_asu(double x) { uint64_t u; __builtin_memcpy(&u, &x, 8); return u; }
 SHUD_PT_FN double shud_pt_asd(uint64_t u) { double x; __builtin_memcpy(&x, &u, 8); return x; }
+// two adjacent table doubles (16-B aligned): one 16-B load on the device (ds_read_b128 from the LDS copy)
+SHUD_PT_FN void shud_pt_ld2(const double *p, double *a, double *b) {
+#ifdef __HIPCC__
+    typedef double shud_pt_v2 __attribute__((ext_vector_type(2)));
+    const shud_pt_v2 v = *(const shud_pt_v2 *)p;
+    *a = v.x;
+    *b = v.y;
+#else
+    *a = p[0];
+    *b = p[1];
+#endif
+}
 
-// log x as hi + *tail (|tail| <= 2^-60 |hi| or so); ix = bits of x, x normal and positive
-SHUD_PT_FN double shud_pt_log(uint64_t ix, double *tail) {
+// log x as hi + *tail (|tail| <= 2^-60 |hi| or so); ix = bits of x, x normal and positive; lt = the log table
+// (shud_pt_logtab or a copy of it)
+SHUD_PT_FN double shud_pt_log(uint64_t ix, double *tail, const double *lt) {
     const uint64_t tmp = ix - SHUD_PT_OFF;
     const int i = (int)((tmp >> 44) & 255);
     const int64_t k = (int64_t)tmp >> 52;                    // arithmetic shift: the exponent relative to OFF
     const uint64_t iz = ix - (tmp & (0xfffULL << 52));
     const double z = shud_pt_asd(iz);
     const double kd = (double)k;
-    const double invc = shud_pt_logtab[i][0], logc = shud_pt_logtab[i][1], logctail = shud_pt_logtab[i][2];
+    double invc, logc;
+    shud_pt_ld2(lt + 4 * i, &invc, &logc);
+    const double logctail = lt[4 * i + 2];
     const double r = __builtin_fma(z, invc, -1.0);           // exact: invc has 9 significant bits
     // k ln2 + log c + r, in double-double
     const double t1 = kd * SHUD_PT_LN2HI + logc;
@@ -82,8 +99,8 @@ SHUD_PT_FN double shud_pt_exp_special(double tmp, uint64_t sbits) {
     return 0x1p-1022 * y;
 }
 
-// exp(x + xtail), |xtail| <= 2^-50 |x| or so; x <= 709 (no overflow path)
-SHUD_PT_FN double shud_pt_exp(double x, double xtail) {
+// exp(x + xtail), |xtail| <= 2^-50 |x| or so; x <= 709 (no overflow path); et = the exp table
+SHUD_PT_FN double shud_pt_exp(double x, double xtail, const double *et) {
     const uint32_t abstop = (uint32_t)(shud_pt_asu(x) >> 52) & 0x7ff;
     bool special = false;
     if (abstop - 0x3c9u >= 0x408u - 0x3c9u) {               // |x| < 2^-54 or |x| >= 512 (0x3c9 = top12(2^-54))
@@ -99,8 +116,9 @@ SHUD_PT_FN double shud_pt_exp(double x, double xtail) {
     r += xtail;
     const int idx = 2 * (int)(ki & 127);
     const uint64_t top = ki << 45;
-    const double tl = shud_pt_asd(shud_pt_exptab[idx]);
-    const uint64_t sbits = shud_pt_exptab[idx + 1] + top;
+    double tl, sb;
+    shud_pt_ld2(et + idx, &tl, &sb);
+    const uint64_t sbits = shud_pt_asu(sb) + top;
     const double r2 = r * r;
     const double C2 = 0.5, C3 = 0x1.5555555555555p-3, C4 = 0x1.5555555555555p-5, C5 = 0x1.1111111111111p-7;
     const double tmp = tl + r + r2 * (C2 + r * C3) + r2 * r2 * (C4 + r * C5);
@@ -109,15 +127,17 @@ SHUD_PT_FN double shud_pt_exp(double x, double xtail) {
     return scale + scale * tmp;
 }
 
-SHUD_PT_FN double shud_pow_tab(double x, double y) {
+SHUD_PT_FN double shud_pow_tab_t(double x, double y, const double *lt, const double *et) {
     uint64_t ix = shud_pt_asu(x);
     if (ix < 0x0010000000000000ULL) {                        // subnormal base (cold): normalise
         ix = shud_pt_asu(x * 0x1p52);
         ix -= 52ULL << 52;
     }
     double lo;
-    const double hi = shud_pt_log(ix, &lo);
+    const double hi = shud_pt_log(ix, &lo, lt);
     const double ehi = y * hi;
     const double elo = y * lo + __builtin_fma(y, hi, -ehi);
-    return shud_pt_exp(ehi, elo);
+    return shud_pt_exp(ehi, elo, et);
 }
+// with the tables in __constant__ memory (device) / static arrays (host)
+SHUD_PT_FN double shud_pow_tab(double x, double y) { return shud_pow_tab_t(x, y, shud_pt_logtab, shud_pt_exptab); }

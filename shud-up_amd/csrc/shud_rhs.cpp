@@ -25,6 +25,8 @@
 #include <vector>
 
 #include "shud_handle.h"
+#define SHUD_PT_HOST_TABLES           // the pow_tab tables as host arrays, uploaded with the class table
+#include "shud_pow_tab.h"
 
 using namespace shud;
 
@@ -435,6 +437,12 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         t[CF_r_Sy] = 1. / t[CF_Sy];
         for (int f = 0; f < CF_COUNT; f++) ctab[(size_t)c * CF_STRIDE + f] = t[f];
     }
+    // pow_tab's tables (shud_pow_tab.h) after the class table, 16-B aligned: one buffer, one LDS copy per workgroup
+    const int pt_off = ((int)ctab.size() + 1) & ~1;
+    ctab.resize((size_t)pt_off + kPowTabDoubles, 0.0);
+    static_assert(kPowTabDoubles == 4 * SHUD_PT_LOG_N + 2 * SHUD_PT_EXP_N, "pow_tab table size");
+    memcpy(&ctab[pt_off], shud_pt_logtab, sizeof shud_pt_logtab);
+    memcpy(&ctab[pt_off + 4 * SHUD_PT_LOG_N], shud_pt_exptab, sizeof shud_pt_exptab);
     std::vector<double2> zz(NE), ged(3 * (size_t)NE);
     std::vector<int4> meta(NE);
     std::vector<int> sfirst(NE);
@@ -459,7 +467,7 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     if ((rc = h->upload(&ged_d, ged.data(), ged.size()))) return rc;
     if ((rc = h->upload(&area_d, m->area, NE))) return rc;
     if ((rc = h->upload(&sf_d, sfirst.data(), NE))) return rc;
-    P.ctab = ctab_d; P.ncls = ncls; P.zz = zz_d; P.meta = meta_d; P.ged = ged_d; P.area = area_d;
+    P.ctab = ctab_d; P.ncls = ncls; P.pt_off = pt_off; P.ntab = (int)ctab.size(); P.zz = zz_d; P.meta = meta_d; P.ged = ged_d; P.area = area_d;
     P.seg_first = sf_d;
     // host reciprocals of static geometric divisors for a kernel built with SHUD_RCP (A/B builds)
     const int rcp = shud_ele_rcp_mask();
