@@ -129,6 +129,8 @@ struct DevPacked {
     // nullptr: off (SHUD_RHS_QD=0), the river kernel recomputes them
     double *qdown;          // [nqd]
     int nqd;
+    int qd_pm, qd_pm_fold;  // where the QrivDown blocks sit in the element launch: after this many permille of its
+                            //   element blocks (single launch / folded partition launch; SHUD_QD_POS[_FOLD])
     int lds_big;            // 1: 129..kLdsClassMaxBig classes take the 1024-thread LDS-table kernel (host dispatch)
     // correctly rounded reciprocals of static geometric divisors, uploaded only for a kernel built with the
     // matching SHUD_RCP bit (shud_ele_rcp_mask()): 1 area, 2 Dist2Nabor [3][NE], 4 segment reach BedThick

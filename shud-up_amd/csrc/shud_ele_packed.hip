@@ -180,20 +180,18 @@ __device__ __forceinline__ int tile_of(int per8) { return tile_of(per8, (int)blo
 // QrivDown pre-pass (DevPacked::qdown): nb_q workgroups of the last element launch of an eval compute every local
 // reach's QrivDown (MD_RiverFlux.cpp:5-63; a function of y only, computed once per reach as MD_f.cpp:41-43 does)
 // into an 8-B slot, so the river kernel reads its own and its upstream reaches' values (MD_f.cpp:236-240) instead
-// of recomputing each from a 64-B reach record and two stages.  They ride after the element tiles, in the launch's
-// tail (SHUD_QD_FIRST=1: before them, A/B); nb_q is a multiple of 8, so the element tiles keep their XCD chunks.
-#ifndef SHUD_QD_FIRST
-#define SHUD_QD_FIRST 0
-#endif
+// of recomputing each from a 64-B reach record and two stages.  They occupy blocks [q0, q0 + nb_q) of the launch,
+// among the element tiles (q0 from DevPacked::qd_pm): late enough that the slots are still in L2 when the river
+// kernel reads them, early enough that their dependent loads overlap element work instead of forming the launch's
+// tail.  q0 and nb_q are multiples of 8, so the element tiles keep their XCD chunks.
 template <int MODE>
 __device__ __forceinline__ void qd_pre(const DevMesh &m, const DevPacked &p, const YView &Y, int r);
-// the QrivDown block index of this workgroup, or -1 for an element workgroup
-__device__ __forceinline__ int qd_block(int nb_e, int nb_q) {
-    const int b = (int)blockIdx.x;
-    if (SHUD_QD_FIRST) return b < nb_q ? b : -1;
-    return b >= nb_e ? b - nb_e : -1;
+// block b -> QrivDown block (>= 0, *e untouched) or -1 with *e = the element block ordinal
+__device__ __forceinline__ int qd_split(int b, int nb_q, int q0, int *e) {
+    if (nb_q && b >= q0 && b < q0 + nb_q) return b - q0;
+    *e = b < q0 ? b : b - nb_q;
+    return -1;
 }
-__device__ __forceinline__ int ele_block(int nb_q) { return (int)blockIdx.x - (SHUD_QD_FIRST ? nb_q : 0); }
 
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
 __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, const YView &Y, double *__restrict__ dy,
@@ -203,17 +201,16 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
 __global__ void __launch_bounds__(kEleBS, SHUD_ELE_WAVES)
 shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int i0, int n_compute, int cur,
-                       DevDiag dg, DevLake lk, int per8, int nb_e, int nb_q) {
-    extern __shared__ double lct[];                       // ncls * CF_LDS_STRIDE doubles when LCT
-    if (nb_q) {
-        const int qb = qd_block(nb_e, nb_q);
-        if (qb >= 0) {
-            const int r = qb * kEleBS + (int)threadIdx.x;
-            if (r < p.nqd) qd_pre<MODE>(m, p, Y, r);
-            return;
-        }
+                       DevDiag dg, DevLake lk, int per8, int nb_q, int q0) {
+    extern __shared__ double lct[];                       // ntab doubles (class table + pow tables) when LCT
+    int eb = (int)blockIdx.x;
+    const int qb = qd_split((int)blockIdx.x, nb_q, q0, &eb);
+    if (qb >= 0) {
+        const int r = qb * kEleBS + (int)threadIdx.x;
+        if (r < p.nqd) qd_pre<MODE>(m, p, Y, r);
+        return;
     }
-    const int i = i0 + tile_of(per8, ele_block(nb_q)) * kEleBS + (int)threadIdx.x;   // elements [i0, n_compute)
+    const int i = i0 + tile_of(per8, eb) * kEleBS + (int)threadIdx.x;   // elements [i0, n_compute)
     const bool act = i < n_compute;
     double tv[kTabBatch];
     if (LCT) tab_issue<kEleBS>(p, tv);
@@ -272,17 +269,19 @@ __device__ __forceinline__ void halo_wait(const DevMesh &m, const HaloWait &hw, 
 template <int MODE, bool OPEN, bool FU1>
 __global__ void __launch_bounds__(256, SHUD_ELE_WAVES)
 shud_ele_kernel_packed_fold(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int n_int, int n_all, int cur,
-                            DevDiag dg, int per8, int nb_int, HaloWait hw, int nb_eb) {
+                            DevDiag dg, int per8, int nb_int, HaloWait hw, int nb_q, int q0) {
     extern __shared__ double lct[];
     const DevLake lk{};
-    if ((int)blockIdx.x >= nb_eb) {                           // QrivDown blocks (after the boundary ones): ghost stages
-        const int r = ((int)blockIdx.x - nb_eb) * 256 + (int)threadIdx.x;
+    int b = (int)blockIdx.x;
+    const int qb = qd_split((int)blockIdx.x, nb_q, q0, &b);
+    if (qb >= 0) {                                            // QrivDown blocks: ghost reaches read the halo
+        const int r = qb * 256 + (int)threadIdx.x;
         halo_wait(m, hw, n_int);
         if (r < p.nqd) qd_pre<MODE>(m, p, Y, r);
         return;
     }
-    if ((int)blockIdx.x < nb_int) {
-        const int i = tile_of(per8) * 256 + (int)threadIdx.x;
+    if (b < nb_int) {
+        const int i = tile_of(per8, b) * 256 + (int)threadIdx.x;
         const bool act = i < n_int;
         double tv[kTabBatch];
         tab_issue<256>(p, tv);
@@ -293,7 +292,7 @@ shud_ele_kernel_packed_fold(DevMesh m, DevPacked p, YView Y, double *__restrict_
         if (act) ele_body<MODE, OPEN, false, FU1, true, false, false>(m, p, Y, dy, i, cur, dg, lk, lct, own);
         return;
     }
-    const int i = n_int + ((int)blockIdx.x - nb_int) * 256 + (int)threadIdx.x;
+    const int i = n_int + (b - nb_int) * 256 + (int)threadIdx.x;
     const bool act = i < n_all;
     double tv[kTabBatch];
     tab_issue<256>(p, tv);
@@ -958,15 +957,21 @@ static void launch_big(const DevMesh &m, const DevPacked &p, const YView &Y, dou
     hipLaunchKernelGGL(fn, dim3(nb), dim3(1024), lds, s, m, p, Y, dy, i0, i1, cur, dg, lk, nb / 8);
 }
 
+// first block of the QrivDown workgroups: pm permille of the nb element blocks before them, rounded down to 8
+static int qd_start(int nb, int pm) {
+    const long long q = (long long)nb * std::min(std::max(pm, 0), 1000) / 1000;
+    return (int)(q / 8 * 8);
+}
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
 static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1, int cur,
                      const DevDiag &dg, const DevLake &lk, hipStream_t s, int nq = 0) {
     int nb = (i1 - i0 + kEleBS - 1) / kEleBS;
     nb = (nb + 7) / 8 * 8;                  // block_id<1> deals blocks to XCDs in contiguous chunks
     const int nbq = nq > 0 ? ((nq + kEleBS - 1) / kEleBS + 7) / 8 * 8 : 0;
+    const int q0 = qd_start(nb, p.qd_pm);
     const size_t lds = LCT ? (size_t)p.ntab * sizeof(double) : 0;
     hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH>), dim3(nb + nbq), dim3(kEleBS), lds, s,
-                       m, p, Y, dy, i0, i1, cur, dg, lk, nb / 8, nb, nbq);
+                       m, p, Y, dy, i0, i1, cur, dg, lk, nb / 8, nbq, q0);
 }
 
 bool launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1,
@@ -1012,11 +1017,13 @@ bool launch_element_kernel_packed_fold(const DevMesh &m, const DevPacked &p, con
                                        const HaloWait &hw, hipStream_t s, bool with_qd) {
     if (n_int <= 0 || n_all <= n_int || p.ncls > LDS_CLS_MAX) return false;
     const int nb_int = ((n_int + 255) / 256 + 7) / 8 * 8, nb_b = (n_all - n_int + 255) / 256;
-    const int nbq = (with_qd && p.qdown && p.nqd > 0) ? (p.nqd + 255) / 256 : 0;
+    const int nbq = (with_qd && p.qdown && p.nqd > 0) ? ((p.nqd + 255) / 256 + 7) / 8 * 8 : 0;
+    // QrivDown blocks among the interior tiles (they wait for the halo like the boundary ones: it has normally
+    // arrived long before), pm of the interior blocks before them
+    const int q0 = qd_start(nb_int, p.qd_pm_fold);
     const size_t lds = (size_t)p.ntab * sizeof(double);
 #define LF(MO, OP, FU) hipLaunchKernelGGL((shud_ele_kernel_packed_fold<MO, OP, FU>), dim3(nb_int + nb_b + nbq), dim3(256), \
-                                          lds, s, m, p, Y, dy, n_int, n_all, cur, dg, nb_int / 8, nb_int, hw,          \
-                                          nb_int + nb_b)
+                                          lds, s, m, p, Y, dy, n_int, n_all, cur, dg, nb_int / 8, nb_int, hw, nbq, q0)
     if (mode == 0) {
         if (open) { if (fu_unit) LF(0, true, true); else LF(0, true, false); }
         else { if (fu_unit) LF(0, false, true); else LF(0, false, false); }

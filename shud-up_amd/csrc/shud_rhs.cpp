@@ -600,6 +600,8 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         if ((rc = h->upload(&P.qdown, (const double *)nullptr, NR))) return rc;
         P.nqd = NR;
     }
+    P.qd_pm = getenv("SHUD_QD_POS") ? atoi(getenv("SHUD_QD_POS")) : 1000;
+    P.qd_pm_fold = getenv("SHUD_QD_POS_FOLD") ? atoi(getenv("SHUD_QD_POS_FOLD")) : 1000;
     h->n_classes = ncls;
     h->packed = true;
     return 0;
