@@ -184,8 +184,10 @@ __device__ __forceinline__ int tile_of(int per8) { return tile_of(per8, (int)blo
 // among the element tiles (q0 from DevPacked::qd_pm): late enough that the slots are still in L2 when the river
 // kernel reads them, early enough that their dependent loads overlap element work instead of forming the launch's
 // tail.  q0 and nb_q are multiples of 8, so the element tiles keep their XCD chunks.
-template <int MODE>
-__device__ __forceinline__ void qd_pre(const DevMesh &m, const DevPacked &p, const YView &Y, int r);
+struct HaloWait;
+template <int MODE, bool HALO>
+__device__ __forceinline__ void qd_pre(const DevMesh &m, const DevPacked &p, const YView &Y, int r, int n_int,
+                                       const HaloWait *hw);
 // block b -> QrivDown block (>= 0, *e untouched) or -1 with *e = the element block ordinal
 __device__ __forceinline__ int qd_split(int b, int nb_q, int q0, int *e) {
     if (nb_q && b >= q0 && b < q0 + nb_q) return b - q0;
@@ -207,7 +209,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     const int qb = qd_split((int)blockIdx.x, nb_q, q0, &eb);
     if (qb >= 0) {
         const int r = qb * kEleBS + (int)threadIdx.x;
-        if (r < p.nqd) qd_pre<MODE>(m, p, Y, r);
+        if (r < p.nqd) qd_pre<MODE, false>(m, p, Y, r, 0, nullptr);
         return;
     }
     const int i = i0 + tile_of(per8, eb) * kEleBS + (int)threadIdx.x;   // elements [i0, n_compute)
@@ -274,10 +276,9 @@ shud_ele_kernel_packed_fold(DevMesh m, DevPacked p, YView Y, double *__restrict_
     const DevLake lk{};
     int b = (int)blockIdx.x;
     const int qb = qd_split((int)blockIdx.x, nb_q, q0, &b);
-    if (qb >= 0) {                                            // QrivDown blocks: ghost reaches read the halo
+    if (qb >= 0) {                                            // QrivDown blocks: only ghost-touching waves wait
         const int r = qb * 256 + (int)threadIdx.x;
-        halo_wait(m, hw, n_int);
-        if (r < p.nqd) qd_pre<MODE>(m, p, Y, r);
+        qd_pre<MODE, true>(m, p, Y, r < p.nqd ? r : -1, n_int, &hw);
         return;
     }
     if (b < nb_int) {
@@ -680,14 +681,24 @@ __device__ __forceinline__ double riv_down_outlet(const RivP &q, double uq, cons
     return riv_down_p(q, uq, g, 0., 0., 0.);
 }
 // QrivDown of local reach r (owned or ghost) into its slot: the river kernel's own-reach term, operand for operand
-// (a ghost reach whose downstream is not local carries the outlet code on its record; its slot is never read)
-template <int MODE>
-__device__ __forceinline__ void qd_pre(const DevMesh &m, const DevPacked &p, const YView &Y, int r) {
-    const RivP q = riv_load(p, r);
+// (a ghost reach whose downstream is not local carries the outlet code on its record; its slot is never read).
+// HALO (the folded partition launch): a wave with a lane whose reach or downstream is a ghost takes the halo
+// wait (poll + agent acquire, which invalidates the CU's L1) before its stage loads; the others — nearly all —
+// read only owned stages and skip it.  r < 0: an idle lane (still reaches the wave-wide ballot).
+template <int MODE, bool HALO>
+__device__ __forceinline__ void qd_pre(const DevMesh &m, const DevPacked &p, const YView &Y, int r, int n_int,
+                                       const HaloWait *hw) {
+    const int rr = r < 0 ? 0 : r;
+    const RivP q = riv_load(p, rr);
+    const int d = q.down >= 0 ? q.down : rr;                    // clamped: unconditional loads
+    if (HALO) {
+        const bool ghost = r >= 0 && (r >= Y.n_own_riv || d >= Y.n_own_riv);
+        if (__builtin_amdgcn_ballot_w64(ghost)) halo_wait(m, *hw, n_int);
+    }
+    if (r < 0) return;
     double yg;
     const double ur = riv_stage_p<MODE>(m, Y, r, q.bc, &yg);
     const RivGeom g = riv_geom_p(q, yg);
-    const int d = q.down >= 0 ? q.down : r;                     // clamped: unconditional loads
     const double2 bd = p.rv[4 * (size_t)d + 1], dd = p.rv[4 * (size_t)d + 3];
     double ydg;
     const double ud = riv_stage_p<MODE>(m, Y, d, rv_ib(dd.y).y, &ydg);
