@@ -116,6 +116,13 @@ constexpr int kEleBS = SHUD_ELE_BS;
 #ifndef SHUD_EABL
 #define SHUD_EABL 0
 #endif
+// SHUD_REP1 (default): f_etFlux's three conditions (negative flux, NaN, eta > 2 ETP) are collected in a lane bit mask
+// and reported together — one ballot per wave when none fired (the common case) instead of three; the same flags,
+// first indices and warning count (atomics commute).  (Deferring all five conditions to the end of the body kept the
+// mask live across the edge loop: 85 VGPRs, 5 waves/SIMD.)  0: report_w at each condition (A/B).
+#ifndef SHUD_REP1
+#define SHUD_REP1 1
+#endif
 // pow_tab's tables read from the workgroup's LDS copy (default) or gathered from the class-table buffer in HBM/L2
 // (SHUD_PT_LDS=0, A/B)
 #ifndef SHUD_PT_LDS
@@ -346,6 +353,13 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     const double etp = stl.y;
     const double2 fu = own.fu;
     const double2 csv = own.csv;
+    // REPORT: an error / warning condition, reported now; REPORT_ET: one of f_etFlux's, collected (SHUD_REP1)
+#define REPORT(c, bit, slot, cnt) do { if (!(SHUD_EABL & 32)) report_w(m.err, (c), (bit), (slot), i, (cnt)); } while (0)
+#define REPORT_ET(c, bit, slot, cnt) do {                                                                       \
+        if (SHUD_EABL & 32) break;                                                                          \
+        if (SHUD_REP1) rep |= (c) ? (uint32_t)(bit) : 0u;                                                   \
+        else report_w(m.err, (c), (bit), (slot), i, (cnt));                                                 \
+    } while (0)
 #define CL(f) (LCT ? lct[cid * CF_LDS_STRIDE + CF_##f] : p.ctab[cid * CF_STRIDE + CF_##f])
 #define CDIV(a, F) CDIV_(a, CL(F), CL(r_##F))
 
@@ -362,7 +376,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
         ekh = CL(KsatH); deficit = 0.; satn = 1.; theta = CL(ThetaS); satkr = 1.0;
     } else {
         ekh = eff_kh(ugw, aq, CL(macD), CL(macKsatH), CL(vAreaF), CL(KsatH));
-        if (!(SHUD_EABL & 32)) report_w(m.err, ekh < 0. || ekh > 1e9, 0x02u, 1, i);
+        REPORT(ekh < 0. || ekh > 1e9, 0x02u, 1, false);
         deficit = aq - ugw;
         const double ThS = CL(ThetaS), ThR = CL(ThetaR);
         if (deficit <= 0.) { deficit = 0.; satn = 1.; theta = ThS; }
@@ -406,14 +420,18 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
             else { Tg = 0.; Tu = rmin(rmax(0., uus), ibeta * (ptr - eic)) * pj * va; }
         } else { Tg = Tu = eic = 0.; }
         const double trans = Tg + Tu, evapo = Eu + Eg + Es, eta = eic + evapo + trans;
-        if (!(SHUD_EABL & 32)) report_w(m.err, eta > etp * 2., 0x10u, 4, i, true);   // printf warning, MD_ET.cpp:391-393
+        uint32_t rep = 0;
+        REPORT_ET(eta > etp * 2., 0x10u, 4, true);        // printf warning, MD_ET.cpp:391-393
         // CheckNonNegative (functions.cpp:148-154): x < 0 || isnan || isinf || |x - NA| < ZERO is exactly
         // "NaN, an infinity, or a negative normal/subnormal" (-0.0 passes; x ~ -9999 is negative): one
         // v_cmp_class per value
         const bool neg = bad_nonneg(Es) || bad_nonneg(Eu) || bad_nonneg(Eg) || bad_nonneg(Tu) || bad_nonneg(Tg);
-        if (!(SHUD_EABL & 32)) {
-            report_w(m.err, neg, 0x04u, 2, i);
-            report_w(m.err, !neg && (nan_or_inf(eta) || nan_or_inf(evapo) || nan_or_inf(trans)), 0x08u, 3, i);
+        REPORT_ET(neg, 0x04u, 2, false);
+        REPORT_ET(!neg && (nan_or_inf(eta) || nan_or_inf(evapo) || nan_or_inf(trans)), 0x08u, 3, false);
+        if (SHUD_REP1 && __builtin_amdgcn_ballot_w64(rep != 0)) {
+            report_w(m.err, rep & 0x04u, 0x04u, 2, i);
+            report_w(m.err, rep & 0x08u, 0x08u, 3, i);
+            report_w(m.err, rep & 0x10u, 0x10u, 4, i, true);
         }
         if (DIAG) { dg.q_es[i] = Es; dg.q_eu[i] = Eu; dg.q_eg[i] = Eg; dg.q_tu[i] = Tu; dg.q_tg[i] = Tg;
                     dg.q_eta[i] = eta; dg.i_beta[i] = ibeta; }
@@ -608,7 +626,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     }
     if (DIAG && is_lake)
         for (int j = 0; j < 3; j++) { dg.qele_surf[j * NEl + i] = 0.; dg.qele_sub[j * NEl + i] = 0.; }
-    if (MODE == 0 && !(SHUD_EABL & 32)) report_w(m.err, nan_q, 0x01u, 0, i);   // CheckNANij, MD_f.cpp:73-74
+    if (MODE == 0) REPORT(nan_q, 0x01u, 0, false);         // CheckNANij, MD_f.cpp:73-74
 
     // ---- f_applyDY element part (MD_f.cpp:88-150 / MD_f_omp.cpp:26-46) ----
 #if !SHUD_AREA_EARLY
@@ -633,6 +651,8 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     __builtin_nontemporal_store(dsf, atw(dy, o8));
     __builtin_nontemporal_store(dgw, atw(dy + 2 * (size_t)nown, o8));
     if (DIAG) { dg.qele_surf_tot[i] = sumsurf; dg.qele_sub_tot[i] = sumsub; }
+#undef REPORT
+#undef REPORT_ET
 }
 
 // ===================================================================================
