@@ -726,9 +726,10 @@ def pmc_traffic(NE):
 def many_class_timing(gm, y, mode, dev, steps):
     """The same syn-10M mesh with per-element calibrated parameters: KsatH perturbed by (1 + 1e-7 k), k =
     element mod 400, so the distinct parameter tuples (classes) grow from 33 to 13,200 — more than the 128 one
-    workgroup's LDS copy of the class table holds.  "auto": the layout the handle picks (the SoA kernel);
-    "l2_class_table": the packed layout with its class table read from L2 (SHUD_RHS_L2_CLASS=1).  Timed like
-    the headline (device-resident y, K evals)."""
+    workgroup's LDS copy of the class table holds.  "auto": the layout the handle picks (the hybrid layout: KsatH
+    streamed per element, 33 classes in LDS); "l2_class_table": the packed layout with its class table read from L2
+    (SHUD_RHS_HYB=0, SHUD_RHS_L2_CLASS=1); "soa": the SoA kernel (SHUD_RHS_HYB=0).  Timed like the headline
+    (device-resident y, K evals)."""
     import copy
     import torch
     from shud_rhs import runtime
@@ -739,13 +740,14 @@ def many_class_timing(gm, y, mode, dev, steps):
     m2 = copy.copy(gm)
     m2.par = dict(gm.par)
     m2.par["KsatH"] = base * (1.0 + 1e-7 * (np.arange(gm.num_ele) % 400))
-    for name, env in (("auto", None), ("l2_class_table", "1")):
-        if env:
-            os.environ["SHUD_RHS_L2_CLASS"] = env
+    for name, env in (("auto", {}), ("l2_class_table", {"SHUD_RHS_HYB": "0", "SHUD_RHS_L2_CLASS": "1"}),
+                      ("soa", {"SHUD_RHS_HYB": "0"})):
+        os.environ.update(env)
         try:
             h = runtime.RhsHandle(m2, mode=mode, device=dev, stream=torch.cuda.current_stream().cuda_stream)
         finally:
-            os.environ.pop("SHUD_RHS_L2_CLASS", None)
+            for k in env:
+                os.environ.pop(k, None)
         h.set_step_inputs()
         lay = h.layout()
         for _ in range(3):
@@ -759,9 +761,10 @@ def many_class_timing(gm, y, mode, dev, steps):
         dt = time.perf_counter() - t0
         me, mr, mv, n = h.timing_read()
         h.close()
-        res[name] = {"layout": "packed" if lay["packed"] else "soa", "n_classes": 13200 if not lay["packed"]
-                     else lay["n_classes"], "value": gm.num_ele * steps / dt, "ms_per_step": dt / steps * 1e3,
-                     "ele_kernel_ms": me, "riv_kernel_ms": mr}
+        res[name] = {"layout": ("hybrid" if lay.get("streamed_fields") else "packed") if lay["packed"] else "soa",
+                     "n_classes": 13200 if not lay["packed"] else lay["n_classes"],
+                     "streamed_fields": lay.get("streamed_fields", 0), "value": gm.num_ele * steps / dt,
+                     "ms_per_step": dt / steps * 1e3, "ele_kernel_ms": me, "riv_kernel_ms": mr}
     torch.cuda.empty_cache()
     return res
 

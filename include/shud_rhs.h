@@ -185,6 +185,10 @@ long long shud_rhs_num_calls(shud_rhs_t h);  /* Model_Data::nFCall */
 /* device layout chosen at create: *packed = 1 when per-element parameters were folded into
  * *n_classes distinct parameter tuples (the fast element kernel); 0 = plain SoA kernel */
 int  shud_rhs_layout(shud_rhs_t h, int *packed, int *n_classes);
+/* hybrid layout of a packed handle: *n_streamed class fields (of KsatH, macD, macKsatH, vAreaF, KsatV, Sy, RzD,
+ * depression, Rough) are streamed per element because the full parameter tuples exceed one workgroup's LDS class
+ * table (per-element-calibrated models); 0 = every field from the class table */
+int  shud_rhs_layout_streamed(shud_rhs_t h, int *n_streamed);
 int  shud_rhs_destroy(shud_rhs_t h);
 const char *shud_rhs_last_error_string(void);
 

@@ -87,12 +87,19 @@ constexpr int kPowTabDoubles = 4 * 256 + 2 * 128;
 // most classes a 1024-thread workgroup stages in LDS ((560 x 33 + 1280) x 8 B = 154 KiB of the CU's 160 KiB: one
 // workgroup per CU, 4 waves/SIMD) — models with 129..560 distinct parameter tuples
 constexpr int kLdsClassMaxBig = 560;
+// hybrid layout: at most this many class fields streamed per element (DevPacked::hv)
+constexpr int kHybMax = 4;
 
 struct DevPacked {
     const double *ctab;     // [ncls][CF_STRIDE] record-major: one class's fields share 2-3 cache lines; then, from
                             //   double pt_off (even: 16-B aligned), pow_tab's log and exp tables (kPowTabDoubles)
     int ncls;
     int pt_off, ntab;       // ntab = pt_off + kPowTabDoubles: the doubles a workgroup copies into LDS
+    // hybrid layout (per-element-calibrated models): nh class fields streamed per element instead of read from the
+    // class table — hv[hs * i + hslot1[f] - 1] for field f with hslot1[f] > 0 (hs = 2 or 4 doubles per element)
+    const double *hv;
+    int nh, hs;
+    signed char hslot1[CF_NPRIMARY];
     const double2 *zz;      // {z_surf, z_bottom}  (aquifer_depth == z_surf - z_bottom, checked at create)
     const int4 *meta;       // {nabr0, nabr1, nabr2, cf}: cf bits 0-7 iBC (int8), 8-9 iSS class,
                             //   10-15 #river segments, 16-30 class id, 31 lake element

@@ -202,12 +202,14 @@ __device__ __forceinline__ int qd_split(int b, int nb_q, int q0, int *e) {
     return -1;
 }
 
-template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, bool HYB = false>
 __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, const YView &Y, double *__restrict__ dy,
                                          int i, int cur, const DevDiag &dg, const DevLake &lk, const double *lct,
                                          const OwnRec &own);
 
-template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
+// HYB: the hybrid layout (DevPacked::hv): the streamed class fields come from the element's (and its neighbours')
+// per-element record, the rest from the LDS class table
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, bool HYB = false>
 __global__ void __launch_bounds__(kEleBS, SHUD_ELE_WAVES)
 shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int i0, int n_compute, int cur,
                        DevDiag dg, DevLake lk, int per8, int nb_q, int q0) {
@@ -229,7 +231,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         tab_store<kEleBS>(p, tv, lct);
         __syncthreads();
     }
-    if (act) ele_body<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH>(m, p, Y, dy, i, cur, dg, lk, lct, own);
+    if (act) ele_body<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH, HYB>(m, p, Y, dy, i, cur, dg, lk, lct, own);
 }
 
 // 129..kLdsClassMaxBig classes: the same body with the class table in LDS, staged by 1024-thread workgroups (one
@@ -333,7 +335,20 @@ __global__ void shud_copy_f64_kernel(double *__restrict__ dst, const double *__r
         dst[k] = src[k];
 }
 
-template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
+// the streamed value of field slot k (1-based, uniform) from a per-element record of up to 4 doubles
+__device__ __forceinline__ double hsel(const double (&v)[4], int k) {
+    return k == 1 ? v[0] : k == 2 ? v[1] : k == 3 ? v[2] : v[3];
+}
+__device__ __forceinline__ void hload(const DevPacked &p, int i, double (&v)[4]) {
+    const double2 a = *(const double2 *)(p.hv + (size_t)p.hs * i);
+    v[0] = a.x; v[1] = a.y; v[2] = 0.; v[3] = 0.;
+    if (p.hs == 4) {
+        const double2 b = *(const double2 *)(p.hv + (size_t)p.hs * i + 2);
+        v[2] = b.x; v[3] = b.y;
+    }
+}
+
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, bool HYB>
 __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, const YView &Y, double *__restrict__ dy,
                                          int i, int cur, const DevDiag &dg, const DevLake &lk, const double *lct,
                                          const OwnRec &own) {
@@ -362,6 +377,12 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     } while (0)
 #define CL(f) (LCT ? lct[cid * CF_LDS_STRIDE + CF_##f] : p.ctab[cid * CF_STRIDE + CF_##f])
 #define CDIV(a, F) CDIV_(a, CL(F), CL(r_##F))
+    // HYB: CLH(f) for a field the hybrid layout may stream (uniform test of its slot), CDIV_SY: a / Sy with Sy
+    // streamed takes the IEEE division (the class reciprocal would be another class's)
+    double hvo[4] = {0., 0., 0., 0.};
+    if (HYB) hload(p, i, hvo);
+#define CLH(f) ((HYB && p.hslot1[CF_##f]) ? hsel(hvo, p.hslot1[CF_##f]) : CL(f))
+#define CDIV_SY(a) ((HYB && p.hslot1[CF_Sy]) ? SDIV(a, hsel(hvo, p.hslot1[CF_Sy])) : CDIV(a, Sy))
 
     // ---- f_update ----
     double usf = ysf_raw, uus = yus_raw;
@@ -373,9 +394,9 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     // ---- updateElement (Element.cpp:347-384); pure function of the state, hoisted above f_etFlux ----
     double ekh, deficit, theta, satn, satkr;
     if (is_lake) {                                // updateLakeElement (Element.cpp:336-346)
-        ekh = CL(KsatH); deficit = 0.; satn = 1.; theta = CL(ThetaS); satkr = 1.0;
+        ekh = CLH(KsatH); deficit = 0.; satn = 1.; theta = CL(ThetaS); satkr = 1.0;
     } else {
-        ekh = eff_kh(ugw, aq, CL(macD), CL(macKsatH), CL(vAreaF), CL(KsatH));
+        ekh = eff_kh(ugw, aq, CLH(macD), CLH(macKsatH), CLH(vAreaF), CLH(KsatH));
         REPORT(ekh < 0. || ekh > 1e9, 0x02u, 1, false);
         deficit = aq - ugw;
         const double ThS = CL(ThetaS), ThR = CL(ThetaR);
@@ -416,7 +437,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
         }
         if (lai_on) {                                                // LAI > ZERO
             if (eic >= ptr) { Tg = Tu = 0.; eic = ptr * pj * va; }
-            else if (ugw > aq - CL(RzD)) { Tg = rmin(rmax(0., ugw), (ptr - eic)) * pj * va; Tu = 0.; }
+            else if (ugw > aq - CLH(RzD)) { Tg = rmin(rmax(0., ugw), (ptr - eic)) * pj * va; Tu = 0.; }
             else { Tg = 0.; Tu = rmin(rmax(0., uus), ibeta * (ptr - eic)) * pj * va; }
         } else { Tg = Tu = eic = 0.; }
         const double trans = Tg + Tu, evapo = Eu + Eg + Es, eta = eic + evapo + trans;
@@ -453,7 +474,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
             else ek = satkr * infK * CL(omh);
             qi = rmin(av, rmax(0., grad * ek));
         }
-        const double KV = CL(KsatV);                               // meanHarmonic, Equations.hpp:45-48
+        const double KV = CLH(KsatV);                              // meanHarmonic, Equations.hpp:45-48
         if (!(ugw > aq - infD && uus < deficit)) {
             double grad = 0.;
             if (theta > ThR && !(uus <= K_EPSILON)) {
@@ -474,10 +495,10 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     // dgw = (recharge - exfil) - Qsub/area - Eg - Tg.  Ends the ET/vertical live ranges early.
     const double dsf_head = snp.x - q_infil + q_exfil;
     const double dgw_head = q_rech - q_exfil;
-    if (i < nown) __builtin_nontemporal_store(is_lake ? 0. : CDIV(q_infil - q_rech - Eu - Tu, Sy), atw(dy + nown, o8));
+    if (i < nown) __builtin_nontemporal_store(is_lake ? 0. : CDIV_SY(q_infil - q_rech - Eu - Tu), atw(dy + nown, o8));
 
     // ---- own river segments (fun_Seg_surface / fun_Seg_sub) and Qe2r (PassValue) ----
-    const double dep = CL(depression), rgh = CL(rough);
+    const double dep = CLH(depression), rgh = CLH(rough);
     double qe2r_surf = 0., qe2r_sub = 0.;
     if (nseg && !(SHUD_EABL & 1)) {
         const double isf_seg = rmax(0., usf - q_infil + q_exfil);
@@ -554,6 +575,9 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
         double qsf = 0., qsb = 0.;
         const int cn = cf_class(ncf);
 #define CN(f) (LCT ? lct[cn * CF_LDS_STRIDE + CF_##f] : p.ctab[cn * CF_STRIDE + CF_##f])
+        double hvn[4] = {0., 0., 0., 0.};                 // HYB: the neighbour's streamed fields
+        if (HYB) hload(p, nc, hvn);
+#define CNH(f) ((HYB && p.hslot1[CF_##f]) ? hsel(hvn, p.hslot1[CF_##f]) : CN(f))
         if (LAKE && nb >= 0 && ncf < 0) {                 // bank edge: the neighbour is a lake element
             const int l = lk.lake_of[nb];
             const double zl = lk.bathy_y[lk.bathy_off[l]];               // lake[l].zmin = bathymetry.yi[0]
@@ -567,7 +591,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
             else {
                 const double ymg = (rmax(ugw, 0.) + rmax(yl, 0.)) * .5;
                 const double grad = D2N_DIV(dhg);
-                const double kmean = 0.5 * (ekh + CN(KsatH));            // the lake element's u_effKH = KsatH
+                const double kmean = 0.5 * (ekh + CNH(KsatH));           // the lake element's u_effKH = KsatH
                 q = kmean * grad * ymg * B;
             }
             lk.bank_qs[(size_t)j * NEl + i] = qsf;
@@ -585,7 +609,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
                 const double s = D2N_DIV(dh);
                 if (s > 0 && isf <= 0) qsf = 0.;
                 else if (s < 0 && nsf <= 0) qsf = 0.;
-                else qsf = manning(ym * B, 0.5 * (rgh + CN(rough)), ym, s);   // avgRough, Element.cpp:253
+                else qsf = manning(ym * B, 0.5 * (rgh + CNH(rough)), ym, s);  // avgRough, Element.cpp:253
             }
             const double ugn = ugw_pk<MODE>(m, ngw_raw, cf_ibc(ncf), nb);
             const double zbn = nzz.y;
@@ -594,8 +618,9 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
             if (dhg > 0. && ugw <= 0.02) q = 0.;
             else if (dhg < 0. && ugn <= 0.02) q = 0.;
             else {
-                const double ekn = (SHUD_EABL & 2) ? CN(KsatH)
-                                                   : eff_kh(ugn, zsn - zbn, CN(macD), CN(macKsatH), CN(vAreaF), CN(KsatH));
+                const double ekn = (SHUD_EABL & 2) ? CNH(KsatH)
+                                                   : eff_kh(ugn, zsn - zbn, CNH(macD), CNH(macKsatH), CNH(vAreaF),
+                                                            CNH(KsatH));
                 const double ymg = (rmax(ugw, 0.) + rmax(ugn, 0.)) * .5;
                 const double grad = D2N_DIV(dhg);
                 const double kmean = 0.5 * (ekh + ekn);
@@ -618,6 +643,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
             qsb = q * fu_sub;
         }
 #undef CN
+#undef CNH
 #undef D2N_DIV
         if (MODE == 0) nan_q |= nan_or_inf(qsf) || nan_or_inf(qsb);
         sumsurf += qsf;
@@ -645,9 +671,11 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
 #undef AREA_DIV
     if (iss == 1) dsf += zero_over(area);                     // QSS is never assigned: 0.0 / area
     else if (iss == 2) dgw += zero_over(area);
-    dgw = CDIV(dgw, Sy);
+    dgw = CDIV_SY(dgw);
     if (is_lake) { dsf = 0.; dgw = 0.; }                      // MD_f.cpp:146-150
 #undef CL
+#undef CLH
+#undef CDIV_SY
     __builtin_nontemporal_store(dsf, atw(dy, o8));
     __builtin_nontemporal_store(dgw, atw(dy + 2 * (size_t)nown, o8));
     if (DIAG) { dg.qele_surf_tot[i] = sumsurf; dg.qele_sub_tot[i] = sumsub; }
@@ -993,7 +1021,7 @@ static int qd_start(int nb, int pm) {
     const long long q = (long long)nb * std::min(std::max(pm, 0), 1000) / 1000;
     return (int)(q / 8 * 8);
 }
-template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH>
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, bool HYB = false>
 static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1, int cur,
                      const DevDiag &dg, const DevLake &lk, hipStream_t s, int nq = 0) {
     int nb = (i1 - i0 + kEleBS - 1) / kEleBS;
@@ -1001,7 +1029,8 @@ static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, doubl
     const int nbq = nq > 0 ? ((nq + kEleBS - 1) / kEleBS + 7) / 8 * 8 : 0;
     const int q0 = qd_start(nb, p.qd_pm);
     const size_t lds = LCT ? (size_t)p.ntab * sizeof(double) : 0;
-    hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH>), dim3(nb + nbq), dim3(kEleBS), lds, s,
+    hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH, HYB>), dim3(nb + nbq), dim3(kEleBS),
+                       lds, s,
                        m, p, Y, dy, i0, i1, cur, dg, lk, nb / 8, nbq, q0);
 }
 
@@ -1026,6 +1055,10 @@ bool launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YV
             if (gh) launch_big<MO, OP, DI, FU, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s);                 \
             else launch_big<MO, OP, DI, FU, false>(m, p, Y, dy, i0, i1, cur, dg, lk, s);                   \
         }                                                                                                 \
+        else if (p.ncls <= LDS_CLS_MAX && p.nh) {                                                         \
+            if (gh) launch_p<MO, OP, DI, FU, true, false, true, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s, nq); \
+            else launch_p<MO, OP, DI, FU, true, false, false, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s, nq);   \
+        }                                                                                                 \
         else if (p.ncls <= LDS_CLS_MAX) {                                                                 \
             if (gh) launch_p<MO, OP, DI, FU, true, false, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s, nq); \
             else launch_p<MO, OP, DI, FU, true, false, false>(m, p, Y, dy, i0, i1, cur, dg, lk, s, nq);   \
@@ -1046,7 +1079,7 @@ bool launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YV
 bool launch_element_kernel_packed_fold(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int n_int,
                                        int n_all, int cur, int mode, bool open, bool fu_unit, const DevDiag &dg,
                                        const HaloWait &hw, hipStream_t s, bool with_qd) {
-    if (n_int <= 0 || n_all <= n_int || p.ncls > LDS_CLS_MAX) return false;
+    if (n_int <= 0 || n_all <= n_int || p.ncls > LDS_CLS_MAX || p.nh) return false;
     const int nb_int = ((n_int + 255) / 256 + 7) / 8 * 8, nb_b = (n_all - n_int + 255) / 256;
     const int nbq = (with_qd && p.qdown && p.nqd > 0) ? ((p.nqd + 255) / 256 + 7) / 8 * 8 : 0;
     // QrivDown blocks among the interior tiles (they wait for the halo like the boundary ones: it has normally

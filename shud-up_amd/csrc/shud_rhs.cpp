@@ -380,8 +380,7 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     std::vector<int> cls(NE);
     std::unordered_map<std::string, int> ids;
     const double dep_default = 0.0002;
-    std::vector<double> r(CF_NPRIMARY);
-    for (int i = 0; i < NE; i++) {
+    auto prim = [&](int i, std::vector<double> &r) {
         r[CF_macD] = p->macD[i]; r[CF_macKsatH] = p->macKsatH[i]; r[CF_vAreaF] = p->geo_vAreaF[i];
         r[CF_KsatH] = p->KsatH[i]; r[CF_KsatV] = p->KsatV[i]; r[CF_infKsatV] = p->infKsatV[i];
         r[CF_hAreaF] = p->hAreaF[i]; r[CF_macKsatV] = p->macKsatV[i]; r[CF_ThetaS] = p->ThetaS[i];
@@ -389,6 +388,55 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         r[CF_RzD] = p->RzD[i]; r[CF_VegFrac] = p->VegFrac[i]; r[CF_ImpAF] = p->ImpAF[i];
         r[CF_depression] = m->depression ? m->depression[i] : dep_default;
         r[CF_rough] = m->rough[i];
+    };
+    // the distinct tuples of the fields outside `mask` (mask fields zeroed), counting stops past `cap`
+    auto count_tuples = [&](uint32_t mask, int cap) {
+        std::unordered_map<std::string, int> seen;
+        std::vector<double> r(CF_NPRIMARY);
+        for (int i = 0; i < NE && (int)seen.size() <= cap; i++) {
+            prim(i, r);
+            for (int f = 0; f < CF_NPRIMARY; f++)
+                if (mask >> f & 1) r[f] = 0.;
+            seen.emplace(std::string((const char *)r.data(), r.size() * sizeof(double)), 0);
+        }
+        return (int)seen.size();
+    };
+    // Hybrid layout (per-element-calibrated models): when the full tuples exceed one workgroup's LDS table, stream up
+    // to kHybMax fields per element (8 B each) and keep the rest in the LDS class table — the fields with the most
+    // distinct values first, among those the kernel reads directly (no host-derived class constant depends on them;
+    // Sy's reciprocal is replaced by the IEEE division, the same bits).  SHUD_RHS_HYB=0: off (A/B).
+    uint32_t hmask = 0;
+    {
+        const char *hy = getenv("SHUD_RHS_HYB");
+        const uint32_t streamable = 1u << CF_macD | 1u << CF_macKsatH | 1u << CF_vAreaF | 1u << CF_KsatH |
+                                    1u << CF_KsatV | 1u << CF_Sy | 1u << CF_RzD | 1u << CF_depression | 1u << CF_rough;
+        if (!h->lakeon && !(hy && hy[0] == '0') && count_tuples(0, kLdsClassMax) > kLdsClassMax) {
+            std::vector<std::pair<int, int>> nd;           // (distinct values, field), capped
+            for (int f = 0; f < CF_NPRIMARY; f++) {
+                if (!(streamable >> f & 1)) continue;
+                std::unordered_map<double, int> v;
+                std::vector<double> r(CF_NPRIMARY);
+                for (int i = 0; i < NE && (int)v.size() <= 65536; i++) {
+                    prim(i, r);
+                    v.emplace(r[f], 0);
+                }
+                if (v.size() > 1) nd.push_back({(int)v.size(), f});
+            }
+            std::stable_sort(nd.begin(), nd.end(), [](const std::pair<int, int> &a, const std::pair<int, int> &b) {
+                return a.first > b.first;
+            });
+            for (int k = 0; k < (int)nd.size() && k < kHybMax; k++) {
+                hmask |= 1u << nd[k].second;
+                if (count_tuples(hmask, kLdsClassMax) <= kLdsClassMax) break;
+                if (k + 1 == kHybMax || k + 1 == (int)nd.size()) hmask = 0;     // not enough: no hybrid layout
+            }
+        }
+    }
+    std::vector<double> r(CF_NPRIMARY);
+    for (int i = 0; i < NE; i++) {
+        prim(i, r);
+        for (int f = 0; f < CF_NPRIMARY; f++)
+            if (hmask >> f & 1) r[f] = 0.;
         std::string k((const char *)r.data(), r.size() * sizeof(double));
         auto it = ids.find(k);
         if (it == ids.end()) {
@@ -467,7 +515,22 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     if ((rc = h->upload(&ged_d, ged.data(), ged.size()))) return rc;
     if ((rc = h->upload(&area_d, m->area, NE))) return rc;
     if ((rc = h->upload(&sf_d, sfirst.data(), NE))) return rc;
-    P.ctab = ctab_d; P.ncls = ncls; P.pt_off = pt_off; P.ntab = (int)ctab.size(); P.zz = zz_d; P.meta = meta_d; P.ged = ged_d; P.area = area_d;
+    P.ctab = ctab_d; P.ncls = ncls; P.pt_off = pt_off; P.ntab = (int)ctab.size(); P.zz = zz_d;
+    if (hmask) {                                                     // the streamed fields, per element
+        int nh = 0;
+        for (int f = 0; f < CF_NPRIMARY; f++)
+            if (hmask >> f & 1) P.hslot1[f] = (signed char)++nh;
+        const int hs = nh <= 2 ? 2 : 4;
+        std::vector<double> hv((size_t)hs * NE, 0.0), rr(CF_NPRIMARY);
+        for (int i = 0; i < NE; i++) {
+            prim(i, rr);
+            for (int f = 0; f < CF_NPRIMARY; f++)
+                if (P.hslot1[f]) hv[(size_t)hs * i + P.hslot1[f] - 1] = rr[f];
+        }
+        double *hv_d;
+        if ((rc = h->upload(&hv_d, hv.data(), hv.size()))) return rc;
+        P.hv = hv_d; P.nh = nh; P.hs = hs;
+    } P.meta = meta_d; P.ged = ged_d; P.area = area_d;
     P.seg_first = sf_d;
     // host reciprocals of static geometric divisors for a kernel built with SHUD_RCP (A/B builds)
     const int rcp = shud_ele_rcp_mask();
@@ -1017,6 +1080,12 @@ extern "C" int shud_rhs_eval(shud_rhs_t h, double t, const double *y, double *yd
 }
 
 extern "C" long long shud_rhs_num_calls(shud_rhs_t h) { return h ? h->ncalls : -1; }
+
+extern "C" int shud_rhs_layout_streamed(shud_rhs_t h, int *n_streamed) {
+    if (!h || !n_streamed) return shud_fail(SHUD_ERR_ARG, "null argument");
+    *n_streamed = h->packed ? h->dp.nh : 0;
+    return SHUD_OK;
+}
 
 extern "C" int shud_rhs_layout(shud_rhs_t h, int *packed, int *n_classes) {
     if (!h) return shud_fail(SHUD_ERR_ARG, "null argument");

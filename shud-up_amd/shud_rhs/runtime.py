@@ -114,9 +114,13 @@ class RhsHandle:
         return lib().shud_rhs_num_calls(self.h)
 
     def layout(self):
-        pk, nc = C.c_int(), C.c_int()
+        pk, nc, ns = C.c_int(), C.c_int(), C.c_int()
         _check(lib().shud_rhs_layout(self.h, C.byref(pk), C.byref(nc)), "shud_rhs_layout")
-        return {"packed": bool(pk.value), "n_classes": nc.value}
+        _check(lib().shud_rhs_layout_streamed(self.h, C.byref(ns)), "shud_rhs_layout_streamed")
+        out = {"packed": bool(pk.value), "n_classes": nc.value}
+        if ns.value:
+            out["streamed_fields"] = ns.value
+        return out
 
     def diagnostics(self):
         m = self.model

@@ -304,33 +304,49 @@ def test_syn_10m(oracle_mod):
                       layout="packed")
 
 
-@pytest.mark.parametrize("l2", ["0", "1"])
-def test_many_classes(oracle_mod, monkeypatch, l2):
-    """Per-element calibrated parameters: > 128 distinct parameter tuples.  Default: the SoA kernel; with
+@pytest.mark.parametrize("kind", ["hybrid", "l2", "soa"])
+def test_many_classes(oracle_mod, monkeypatch, kind):
+    """Per-element calibrated parameters: > 128 distinct parameter tuples.  Default: the hybrid layout (KsatH and Sy
+    streamed per element, the rest in the LDS class table); with SHUD_RHS_HYB=0 the SoA kernel, or with
     SHUD_RHS_L2_CLASS=1 the packed kernel reading its class table from L2 (record-major, no LDS copy)."""
-    monkeypatch.setenv("SHUD_RHS_L2_CLASS", l2)
+    if kind != "hybrid":
+        monkeypatch.setenv("SHUD_RHS_HYB", "0")
+        monkeypatch.setenv("SHUD_RHS_L2_CLASS", "1" if kind == "l2" else "0")
     m, y = cases.variant(20000, seed=17)
     m.par["KsatH"] = m.par["KsatH"] * (1.0 + 1e-7 * (np.arange(m.num_ele) % 300))
     m.par["Sy"] = m.par["Sy"] * (1.0 + 1e-9 * (np.arange(m.num_ele) % 7))
+    if kind == "hybrid":
+        lay = _runtime().RhsHandle(m).layout()
+        assert lay["packed"] and lay.get("streamed_fields") == 2 and lay["n_classes"] <= 128, lay
     for mode in (abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP):
         _compare_sequence(m, [y] + cases.states(m, None, 1, seed=3), mode, oracle_mod, ncalls=2,
-                          label=f"many-class l2={l2}", layout="packed" if l2 == "1" else "soa")
+                          label=f"many-class {kind}", layout="soa" if kind == "soa" else "packed")
 
 
-def test_lds_big_class_table(oracle_mod, monkeypatch):
-    """129..600 distinct parameter tuples: the packed kernel with the class table staged in LDS by 1024-thread
-    workgroups (shud_ele_kernel_packed_big), serial and OMP semantics, against the oracle."""
-    monkeypatch.delenv("SHUD_RHS_L2_CLASS", raising=False)
-    rt = _runtime()
-    m, y = cases.variant(20000, seed=17)
-    m.par["KsatH"] = m.par["KsatH"] * (1.0 + 1e-7 * (np.arange(m.num_ele) % 12))     # 33 x 12 tuples
-    h = rt.RhsHandle(m)
-    lay = h.layout()
-    h.close()
-    assert lay["packed"] and 128 < lay["n_classes"] <= 600, lay
-    for mode in (abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP):
-        _compare_sequence(m, [y] + cases.states(m, None, 1, seed=3), mode, oracle_mod, ncalls=2,
-                          label=f"lds-big {lay['n_classes']} classes", layout="packed")
+def _hybrid_model(n=20000, seed=19):
+    """every element its own KsatH, Rough, macD and Sy (four streamed fields, the 32-B per-element record)"""
+    m, y = cases.variant(n, seed=seed)
+    k = np.arange(m.num_ele)
+    m.par["KsatH"] = m.par["KsatH"] * (1.0 + 1e-6 * k / m.num_ele)
+    m.par["macD"] = m.par["macD"] * (1.0 + 1e-3 * ((k * 7) % 11))
+    m.par["Sy"] = m.par["Sy"] * (1.0 + 1e-9 * (k % 13))
+    rough = m.ele["rough"] * (1.0 + 1e-2 * ((k * 3) % 5))
+    m.ele["rough"] = rough
+    nb = m.nabr.reshape(3, -1)          # avgRough = (Rough_i + Rough_j) / 2 (Element.cpp:253), own Rough on a boundary
+    m.ele["avg_rough"] = np.where(nb >= 0, 0.5 * (rough[None, :] + rough[np.maximum(nb, 0)]),
+                                  rough[None, :]).reshape(-1)
+    return m, y
+
+
+@pytest.mark.parametrize("mode", [abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP])
+def test_hybrid_layout(mode, oracle_mod):
+    """The hybrid layout with four streamed fields, each per-element unique or nearly (KsatH, macD, Sy, Rough: the
+    neighbour's streamed KsatH / macD / Rough enter the edge fluxes), against the oracle, 3 stateful calls on 3
+    states, every diagnostic."""
+    m, y = _hybrid_model()
+    lay = _runtime().RhsHandle(m, mode=mode).layout()
+    assert lay["packed"] and lay.get("streamed_fields") == 4, lay
+    _compare_sequence(m, [y] + cases.states(m, None, 2, seed=41), mode, oracle_mod, label="hybrid", layout="packed")
 
 
 @pytest.mark.parametrize("mode", [abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP])
