@@ -116,6 +116,20 @@ def test_cpp_plans_bit_identical(nranks, method):
         _run_ranks(m, [y, workload.random_state(m, seed=5)], locs, mode, ncalls=2)
 
 
+@pytest.mark.parametrize("device_eval", [False, True])
+def test_hybrid_layout_partitions(device_eval):
+    """Per-element-calibrated parameters (the hybrid layout: four class fields streamed per element) on 4 C++-planned
+    ranks: every rank's local mesh chooses its own streamed fields and class table, and the owned DY stays
+    bit-identical to the single GPU (a streamed value and a class-table value are the same bits; Sy's IEEE division
+    equals the class reciprocal's cdiv)."""
+    import test_gpu_parity as tp
+    m, y = tp._hybrid_model(20000, seed=29)
+    ep, _ = partition.cpp_partition(m, 4, partition.PART_AUTO)
+    locs = [partition.CppPlan(m, ep, 4, r).local_model() for r in range(4)]
+    for mode in (0, 1):
+        _run_ranks(m, [y, workload.random_state(m, seed=6)], locs, mode, ncalls=2, device_eval=device_eval)
+
+
 @pytest.mark.parametrize("nranks", [3, 5])
 @pytest.mark.parametrize("seed", [2, 9])
 def test_ragged_random_partitions(nranks, seed):
