@@ -402,33 +402,50 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         return (int)seen.size();
     };
     // Hybrid layout (per-element-calibrated models): when the full tuples exceed one workgroup's LDS table, stream up
-    // to kHybMax fields per element (8 B each) and keep the rest in the LDS class table — the fields with the most
-    // distinct values first, among those the kernel reads directly (no host-derived class constant depends on them;
-    // Sy's reciprocal is replaced by the IEEE division, the same bits).  SHUD_RHS_HYB=0: off (A/B).
+    // to kHybMax fields per element (8 B each) and keep the rest in the LDS class table — the fields that split the
+    // classes of the non-streamable fields the most first, among those the kernel reads directly (no host-derived
+    // class constant depends on them; Sy's reciprocal is replaced by the IEEE division, the same bits).
+    // SHUD_RHS_HYB=0: off (A/B).
     uint32_t hmask = 0;
     {
         const char *hy = getenv("SHUD_RHS_HYB");
         const uint32_t streamable = 1u << CF_macD | 1u << CF_macKsatH | 1u << CF_vAreaF | 1u << CF_KsatH |
                                     1u << CF_KsatV | 1u << CF_Sy | 1u << CF_RzD | 1u << CF_depression | 1u << CF_rough;
-        if (!h->lakeon && !(hy && hy[0] == '0') && count_tuples(0, kLdsClassMax) > kLdsClassMax) {
-            std::vector<std::pair<int, int>> nd;           // (distinct values, field), capped
+        if (!h->lakeon && !(hy && hy[0] == '0') && count_tuples(0, kLdsClassMax) > kLdsClassMax &&
+            count_tuples(streamable, kLdsClassMax) <= kLdsClassMax) {
+            // base classes: the tuples of the fields that cannot be streamed; then, per streamable field, how many
+            // (base class, value) pairs it makes — the fields that split the base classes most are streamed first
+            std::unordered_map<std::string, int> bid;
+            std::vector<int> base(NE);
+            std::vector<double> r(CF_NPRIMARY);
+            for (int i = 0; i < NE; i++) {
+                prim(i, r);
+                for (int f = 0; f < CF_NPRIMARY; f++)
+                    if (streamable >> f & 1) r[f] = 0.;
+                base[i] = bid.emplace(std::string((const char *)r.data(), r.size() * sizeof(double)),
+                                      (int)bid.size()).first->second;
+            }
+            std::vector<std::pair<size_t, int>> split;       // (distinct (base, value) pairs, field)
             for (int f = 0; f < CF_NPRIMARY; f++) {
                 if (!(streamable >> f & 1)) continue;
-                std::unordered_map<double, int> v;
-                std::vector<double> r(CF_NPRIMARY);
-                for (int i = 0; i < NE && (int)v.size() <= 65536; i++) {
+                std::unordered_map<std::string, int> pairs;
+                for (int i = 0; i < NE && pairs.size() <= (size_t)1 << 20; i++) {
                     prim(i, r);
-                    v.emplace(r[f], 0);
+                    char key[12];
+                    memcpy(key, &base[i], 4);
+                    memcpy(key + 4, &r[f], 8);
+                    pairs.emplace(std::string(key, 12), 0);
                 }
-                if (v.size() > 1) nd.push_back({(int)v.size(), f});
+                if (pairs.size() > bid.size()) split.push_back({pairs.size(), f});
             }
-            std::stable_sort(nd.begin(), nd.end(), [](const std::pair<int, int> &a, const std::pair<int, int> &b) {
-                return a.first > b.first;
-            });
-            for (int k = 0; k < (int)nd.size() && k < kHybMax; k++) {
-                hmask |= 1u << nd[k].second;
+            std::stable_sort(split.begin(), split.end(),
+                             [](const std::pair<size_t, int> &a, const std::pair<size_t, int> &b) {
+                                 return a.first > b.first;
+                             });
+            for (int k = 0; k < (int)split.size() && k < kHybMax; k++) {
+                hmask |= 1u << split[k].second;
                 if (count_tuples(hmask, kLdsClassMax) <= kLdsClassMax) break;
-                if (k + 1 == kHybMax || k + 1 == (int)nd.size()) hmask = 0;     // not enough: no hybrid layout
+                if (k + 1 == kHybMax || k + 1 == (int)split.size()) hmask = 0;   // not enough: no hybrid layout
             }
         }
     }
