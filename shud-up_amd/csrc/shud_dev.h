@@ -96,7 +96,7 @@ struct DevPacked {
     int ncls;
     int pt_off, ntab;       // ntab = pt_off + kPowTabDoubles: the doubles a workgroup copies into LDS
     // hybrid layout (per-element-calibrated models): nh class fields streamed per element instead of read from the
-    // class table — hv[hs * i + hslot1[f] - 1] for field f with hslot1[f] > 0 (hs = 2 or 4 doubles per element)
+    // class table — hv[hs * i + hslot1[f] - 1] for field f with hslot1[f] > 0 (hs = 1, 2 or 4 doubles per element)
     const double *hv;
     int nh, hs;
     signed char hslot1[CF_NPRIMARY];

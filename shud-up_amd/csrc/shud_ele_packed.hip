@@ -335,13 +335,27 @@ __global__ void shud_copy_f64_kernel(double *__restrict__ dst, const double *__r
         dst[k] = src[k];
 }
 
-// the streamed value of field slot k (1-based, uniform) from a per-element record of up to 4 doubles
-__device__ __forceinline__ double hsel(const double (&v)[4], int k) {
-    return k == 1 ? v[0] : k == 2 ? v[1] : k == 3 ? v[2] : v[3];
+// the streamed value of field slot k (1-based, wave-uniform) from a per-element record of up to 4 doubles, or the
+// class-table value c when the field is not streamed (k = 0).  Both operands are formed first and the choice is a
+// select on a uniform mask, not a branch: scalar branches around every class-field read split the body into ~70
+// basic blocks and cost more than the selects (profiles/r05/hybrid/).
+__device__ __forceinline__ double hpick(const double (&v)[4], int k, double c) {
+    double r = c;
+    r = k == 1 ? v[0] : r;
+    r = k == 2 ? v[1] : r;
+    r = k == 3 ? v[2] : r;
+    r = k == 4 ? v[3] : r;
+    return r;
 }
+// the element's streamed record: hs = 1 (one field), 2 or 4 doubles
 __device__ __forceinline__ void hload(const DevPacked &p, int i, double (&v)[4]) {
+    v[1] = 0.; v[2] = 0.; v[3] = 0.;
+    if (p.hs == 1) {
+        v[0] = p.hv[i];
+        return;
+    }
     const double2 a = *(const double2 *)(p.hv + (size_t)p.hs * i);
-    v[0] = a.x; v[1] = a.y; v[2] = 0.; v[3] = 0.;
+    v[0] = a.x; v[1] = a.y;
     if (p.hs == 4) {
         const double2 b = *(const double2 *)(p.hv + (size_t)p.hs * i + 2);
         v[2] = b.x; v[3] = b.y;
@@ -381,8 +395,8 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     // streamed takes the IEEE division (the class reciprocal would be another class's)
     double hvo[4] = {0., 0., 0., 0.};
     if (HYB) hload(p, i, hvo);
-#define CLH(f) ((HYB && p.hslot1[CF_##f]) ? hsel(hvo, p.hslot1[CF_##f]) : CL(f))
-#define CDIV_SY(a) ((HYB && p.hslot1[CF_Sy]) ? SDIV(a, hsel(hvo, p.hslot1[CF_Sy])) : CDIV(a, Sy))
+#define CLH(f) (HYB ? hpick(hvo, p.hslot1[CF_##f], CL(f)) : CL(f))
+#define CDIV_SY(a) ((HYB && p.hslot1[CF_Sy]) ? SDIV(a, hpick(hvo, p.hslot1[CF_Sy], 0.)) : CDIV(a, Sy))
 
     // ---- f_update ----
     double usf = ysf_raw, uus = yus_raw;
@@ -577,7 +591,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
 #define CN(f) (LCT ? lct[cn * CF_LDS_STRIDE + CF_##f] : p.ctab[cn * CF_STRIDE + CF_##f])
         double hvn[4] = {0., 0., 0., 0.};                 // HYB: the neighbour's streamed fields
         if (HYB) hload(p, nc, hvn);
-#define CNH(f) ((HYB && p.hslot1[CF_##f]) ? hsel(hvn, p.hslot1[CF_##f]) : CN(f))
+#define CNH(f) (HYB ? hpick(hvn, p.hslot1[CF_##f], CN(f)) : CN(f))
         if (LAKE && nb >= 0 && ncf < 0) {                 // bank edge: the neighbour is a lake element
             const int l = lk.lake_of[nb];
             const double zl = lk.bathy_y[lk.bathy_off[l]];               // lake[l].zmin = bathymetry.yi[0]

@@ -537,7 +537,7 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         int nh = 0;
         for (int f = 0; f < CF_NPRIMARY; f++)
             if (hmask >> f & 1) P.hslot1[f] = (signed char)++nh;
-        const int hs = nh <= 2 ? 2 : 4;
+        const int hs = nh == 1 ? 1 : nh == 2 ? 2 : 4;
         std::vector<double> hv((size_t)hs * NE, 0.0), rr(CF_NPRIMARY);
         for (int i = 0; i < NE; i++) {
             prim(i, rr);
