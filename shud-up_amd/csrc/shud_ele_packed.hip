@@ -336,9 +336,16 @@ __global__ void shud_copy_f64_kernel(double *__restrict__ dst, const double *__r
 }
 
 // the streamed value of field slot k (1-based, wave-uniform) from a per-element record of up to 4 doubles, or the
-// class-table value c when the field is not streamed (k = 0).  Both operands are formed first and the choice is a
-// select on a uniform mask, not a branch: scalar branches around every class-field read split the body into ~70
-// basic blocks and cost more than the selects (profiles/r05/hybrid/).
+// class-table value c when the field is not streamed (k = 0).  SHUD_HYBSEL=0 (default): a uniform branch per read;
+// 1: both operands formed and a select chain on the uniform slot (fewer basic blocks, more VALU: measured slower,
+// profiles/r05/hybrid/).  SHUD_HYBABL (timing only): bit 0 the neighbours' streamed values, bit 1 the element's own,
+// replaced by the class-table value.
+#ifndef SHUD_HYBSEL
+#define SHUD_HYBSEL 0
+#endif
+#ifndef SHUD_HYBABL
+#define SHUD_HYBABL 0
+#endif
 __device__ __forceinline__ double hpick(const double (&v)[4], int k, double c) {
     double r = c;
     r = k == 1 ? v[0] : r;
@@ -346,6 +353,9 @@ __device__ __forceinline__ double hpick(const double (&v)[4], int k, double c) {
     r = k == 3 ? v[2] : r;
     r = k == 4 ? v[3] : r;
     return r;
+}
+__device__ __forceinline__ double hsel(const double (&v)[4], int k) {
+    return k == 1 ? v[0] : k == 2 ? v[1] : k == 3 ? v[2] : v[3];
 }
 // the element's streamed record: hs = 1 (one field), 2 or 4 doubles
 __device__ __forceinline__ void hload(const DevPacked &p, int i, double (&v)[4]) {
@@ -395,8 +405,12 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     // streamed takes the IEEE division (the class reciprocal would be another class's)
     double hvo[4] = {0., 0., 0., 0.};
     if (HYB) hload(p, i, hvo);
-#define CLH(f) (HYB ? hpick(hvo, p.hslot1[CF_##f], CL(f)) : CL(f))
-#define CDIV_SY(a) ((HYB && p.hslot1[CF_Sy]) ? SDIV(a, hpick(hvo, p.hslot1[CF_Sy], 0.)) : CDIV(a, Sy))
+#if SHUD_HYBSEL
+#define CLH(f) ((HYB && !(SHUD_HYBABL & 2)) ? hpick(hvo, p.hslot1[CF_##f], CL(f)) : CL(f))
+#else
+#define CLH(f) ((HYB && !(SHUD_HYBABL & 2) && p.hslot1[CF_##f]) ? hsel(hvo, p.hslot1[CF_##f]) : CL(f))
+#endif
+#define CDIV_SY(a) ((HYB && p.hslot1[CF_Sy]) ? SDIV(a, hsel(hvo, p.hslot1[CF_Sy])) : CDIV(a, Sy))
 
     // ---- f_update ----
     double usf = ysf_raw, uus = yus_raw;
@@ -590,8 +604,12 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
         const int cn = cf_class(ncf);
 #define CN(f) (LCT ? lct[cn * CF_LDS_STRIDE + CF_##f] : p.ctab[cn * CF_STRIDE + CF_##f])
         double hvn[4] = {0., 0., 0., 0.};                 // HYB: the neighbour's streamed fields
-        if (HYB) hload(p, nc, hvn);
-#define CNH(f) (HYB ? hpick(hvn, p.hslot1[CF_##f], CN(f)) : CN(f))
+        if (HYB && !(SHUD_HYBABL & 1)) hload(p, nc, hvn);
+#if SHUD_HYBSEL
+#define CNH(f) ((HYB && !(SHUD_HYBABL & 1)) ? hpick(hvn, p.hslot1[CF_##f], CN(f)) : CN(f))
+#else
+#define CNH(f) ((HYB && !(SHUD_HYBABL & 1) && p.hslot1[CF_##f]) ? hsel(hvn, p.hslot1[CF_##f]) : CN(f))
+#endif
         if (LAKE && nb >= 0 && ncf < 0) {                 // bank edge: the neighbour is a lake element
             const int l = lk.lake_of[nb];
             const double zl = lk.bathy_y[lk.bathy_off[l]];               // lake[l].zmin = bathymetry.yi[0]

@@ -24,10 +24,14 @@ ap.add_argument("--variants", default="soa0,soa3,pk,pk4,pk5",
                      "pk / pkW = packed class-layout kernel (min W waves/SIMD)")
 ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--reps", type=int, default=20)
+ap.add_argument("--many-class", action="store_true",
+                help="KsatH per element (bench.py many_class: 13,200 tuples -> the hybrid layout)")
 a = ap.parse_args()
 m = synth.synth_model(a.n_ele)
 m.step = workload.random_step_inputs(m)
 y = workload.random_state(m)
+if a.many_class:
+    m.par["KsatH"] = m.par["KsatH"] * (1.0 + 1e-7 * (np.arange(m.num_ele) % 400))
 vs = a.variants.split(",")
 
 
