@@ -99,6 +99,7 @@ struct DevPacked {
     // class table — hv[hs * i + hslot1[f] - 1] for field f with hslot1[f] > 0 (hs = 1, 2 or 4 doubles per element)
     const double *hv;
     int nh, hs;
+    int hnb;                // a streamed field is read for the neighbours too (macD, macKsatH, vAreaF, KsatH, Rough)
     signed char hslot1[CF_NPRIMARY];
     const double2 *zz;      // {z_surf, z_bottom}  (aquifer_depth == z_surf - z_bottom, checked at create)
     const int4 *meta;       // {nabr0, nabr1, nabr2, cf}: cf bits 0-7 iBC (int8), 8-9 iSS class,

@@ -202,14 +202,15 @@ __device__ __forceinline__ int qd_split(int b, int nb_q, int q0, int *e) {
     return -1;
 }
 
-template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, bool HYB = false>
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB = 0>
 __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, const YView &Y, double *__restrict__ dy,
                                          int i, int cur, const DevDiag &dg, const DevLake &lk, const double *lct,
                                          const OwnRec &own);
 
 // HYB: the hybrid layout (DevPacked::hv): the streamed class fields come from the element's (and its neighbours')
-// per-element record, the rest from the LDS class table
-template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, bool HYB = false>
+// per-element record, the rest from the LDS class table; 1 = one streamed field (one 8-B value per element, held in
+// one register pair), 2 = two to four
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB = 0>
 __global__ void __launch_bounds__(kEleBS, SHUD_ELE_WAVES)
 shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int i0, int n_compute, int cur,
                        DevDiag dg, DevLake lk, int per8, int nb_q, int q0) {
@@ -372,7 +373,7 @@ __device__ __forceinline__ void hload(const DevPacked &p, int i, double (&v)[4])
     }
 }
 
-template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, bool HYB>
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB>
 __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, const YView &Y, double *__restrict__ dy,
                                          int i, int cur, const DevDiag &dg, const DevLake &lk, const double *lct,
                                          const OwnRec &own) {
@@ -404,13 +405,14 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     // HYB: CLH(f) for a field the hybrid layout may stream (uniform test of its slot), CDIV_SY: a / Sy with Sy
     // streamed takes the IEEE division (the class reciprocal would be another class's)
     double hvo[4] = {0., 0., 0., 0.};
-    if (HYB) hload(p, i, hvo);
+    if (HYB == 1 && !(SHUD_HYBABL & 2)) hvo[0] = p.hv[i];
+    else if (HYB == 2 && !(SHUD_HYBABL & 2)) hload(p, i, hvo);
 #if SHUD_HYBSEL
 #define CLH(f) ((HYB && !(SHUD_HYBABL & 2)) ? hpick(hvo, p.hslot1[CF_##f], CL(f)) : CL(f))
 #else
-#define CLH(f) ((HYB && !(SHUD_HYBABL & 2) && p.hslot1[CF_##f]) ? hsel(hvo, p.hslot1[CF_##f]) : CL(f))
+#define CLH(f) ((HYB && !(SHUD_HYBABL & 2) && p.hslot1[CF_##f]) ? (HYB == 1 ? hvo[0] : hsel(hvo, p.hslot1[CF_##f])) : CL(f))
 #endif
-#define CDIV_SY(a) ((HYB && p.hslot1[CF_Sy]) ? SDIV(a, hsel(hvo, p.hslot1[CF_Sy])) : CDIV(a, Sy))
+#define CDIV_SY(a) ((HYB && p.hslot1[CF_Sy]) ? SDIV(a, HYB == 1 ? hvo[0] : hsel(hvo, p.hslot1[CF_Sy])) : CDIV(a, Sy))
 
     // ---- f_update ----
     double usf = ysf_raw, uus = yus_raw;
@@ -603,12 +605,13 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
         double qsf = 0., qsb = 0.;
         const int cn = cf_class(ncf);
 #define CN(f) (LCT ? lct[cn * CF_LDS_STRIDE + CF_##f] : p.ctab[cn * CF_STRIDE + CF_##f])
-        double hvn[4] = {0., 0., 0., 0.};                 // HYB: the neighbour's streamed fields
-        if (HYB && !(SHUD_HYBABL & 1)) hload(p, nc, hvn);
+        double hvn[4] = {0., 0., 0., 0.};                 // HYB: the neighbour's streamed fields (if it reads any)
+        if (HYB == 1 && !(SHUD_HYBABL & 1) && p.hnb) hvn[0] = p.hv[nc];
+        else if (HYB == 2 && !(SHUD_HYBABL & 1) && p.hnb) hload(p, nc, hvn);
 #if SHUD_HYBSEL
 #define CNH(f) ((HYB && !(SHUD_HYBABL & 1)) ? hpick(hvn, p.hslot1[CF_##f], CN(f)) : CN(f))
 #else
-#define CNH(f) ((HYB && !(SHUD_HYBABL & 1) && p.hslot1[CF_##f]) ? hsel(hvn, p.hslot1[CF_##f]) : CN(f))
+#define CNH(f) ((HYB && !(SHUD_HYBABL & 1) && p.hslot1[CF_##f]) ? (HYB == 1 ? hvn[0] : hsel(hvn, p.hslot1[CF_##f])) : CN(f))
 #endif
         if (LAKE && nb >= 0 && ncf < 0) {                 // bank edge: the neighbour is a lake element
             const int l = lk.lake_of[nb];
@@ -1053,7 +1056,7 @@ static int qd_start(int nb, int pm) {
     const long long q = (long long)nb * std::min(std::max(pm, 0), 1000) / 1000;
     return (int)(q / 8 * 8);
 }
-template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, bool HYB = false>
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB = 0>
 static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1, int cur,
                      const DevDiag &dg, const DevLake &lk, hipStream_t s, int nq = 0) {
     int nb = (i1 - i0 + kEleBS - 1) / kEleBS;
@@ -1087,9 +1090,13 @@ bool launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YV
             if (gh) launch_big<MO, OP, DI, FU, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s);                 \
             else launch_big<MO, OP, DI, FU, false>(m, p, Y, dy, i0, i1, cur, dg, lk, s);                   \
         }                                                                                                 \
+        else if (p.ncls <= LDS_CLS_MAX && p.nh == 1) {                                                    \
+            if (gh) launch_p<MO, OP, DI, FU, true, false, true, 1>(m, p, Y, dy, i0, i1, cur, dg, lk, s, nq); \
+            else launch_p<MO, OP, DI, FU, true, false, false, 1>(m, p, Y, dy, i0, i1, cur, dg, lk, s, nq);   \
+        }                                                                                                 \
         else if (p.ncls <= LDS_CLS_MAX && p.nh) {                                                         \
-            if (gh) launch_p<MO, OP, DI, FU, true, false, true, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s, nq); \
-            else launch_p<MO, OP, DI, FU, true, false, false, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s, nq);   \
+            if (gh) launch_p<MO, OP, DI, FU, true, false, true, 2>(m, p, Y, dy, i0, i1, cur, dg, lk, s, nq); \
+            else launch_p<MO, OP, DI, FU, true, false, false, 2>(m, p, Y, dy, i0, i1, cur, dg, lk, s, nq);   \
         }                                                                                                 \
         else if (p.ncls <= LDS_CLS_MAX) {                                                                 \
             if (gh) launch_p<MO, OP, DI, FU, true, false, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s, nq); \

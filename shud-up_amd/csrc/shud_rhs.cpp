@@ -547,6 +547,7 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         double *hv_d;
         if ((rc = h->upload(&hv_d, hv.data(), hv.size()))) return rc;
         P.hv = hv_d; P.nh = nh; P.hs = hs;
+        P.hnb = (hmask & (1u << CF_macD | 1u << CF_macKsatH | 1u << CF_vAreaF | 1u << CF_KsatH | 1u << CF_rough)) != 0;
     } P.meta = meta_d; P.ged = ged_d; P.area = area_d;
     P.seg_first = sf_d;
     // host reciprocals of static geometric divisors for a kernel built with SHUD_RCP (A/B builds)

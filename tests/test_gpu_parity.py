@@ -304,7 +304,7 @@ def test_syn_10m(oracle_mod):
                       layout="packed")
 
 
-@pytest.mark.parametrize("kind", ["hybrid", "l2", "soa"])
+@pytest.mark.parametrize("kind", ["hybrid1", "hybrid", "l2", "soa"])
 def test_many_classes(oracle_mod, monkeypatch, kind):
     """Per-element calibrated parameters: > 128 distinct parameter tuples.  Default: the hybrid layout (KsatH and Sy
     streamed per element, the rest in the LDS class table); with SHUD_RHS_HYB=0 the SoA kernel, or with
@@ -314,10 +314,12 @@ def test_many_classes(oracle_mod, monkeypatch, kind):
         monkeypatch.setenv("SHUD_RHS_L2_CLASS", "1" if kind == "l2" else "0")
     m, y = cases.variant(20000, seed=17)
     m.par["KsatH"] = m.par["KsatH"] * (1.0 + 1e-7 * (np.arange(m.num_ele) % 300))
-    m.par["Sy"] = m.par["Sy"] * (1.0 + 1e-9 * (np.arange(m.num_ele) % 7))
-    if kind == "hybrid":
+    if kind != "hybrid1":                        # hybrid1: KsatH alone (one streamed field, the 8-B record)
+        m.par["Sy"] = m.par["Sy"] * (1.0 + 1e-9 * (np.arange(m.num_ele) % 7))
+    if kind.startswith("hybrid"):
         lay = _runtime().RhsHandle(m).layout()
-        assert lay["packed"] and lay.get("streamed_fields") == 2 and lay["n_classes"] <= 128, lay
+        assert lay["packed"] and lay.get("streamed_fields") == (1 if kind == "hybrid1" else 2), lay
+        assert lay["n_classes"] <= 128, lay
     for mode in (abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP):
         _compare_sequence(m, [y] + cases.states(m, None, 1, seed=3), mode, oracle_mod, ncalls=2,
                           label=f"many-class {kind}", layout="soa" if kind == "soa" else "packed")
