@@ -309,7 +309,7 @@ def test_many_classes(oracle_mod, monkeypatch, kind):
     """Per-element calibrated parameters: > 128 distinct parameter tuples.  Default: the hybrid layout (KsatH and Sy
     streamed per element, the rest in the LDS class table); with SHUD_RHS_HYB=0 the SoA kernel, or with
     SHUD_RHS_L2_CLASS=1 the packed kernel reading its class table from L2 (record-major, no LDS copy)."""
-    if kind != "hybrid":
+    if not kind.startswith("hybrid"):
         monkeypatch.setenv("SHUD_RHS_HYB", "0")
         monkeypatch.setenv("SHUD_RHS_L2_CLASS", "1" if kind == "l2" else "0")
     m, y = cases.variant(20000, seed=17)
