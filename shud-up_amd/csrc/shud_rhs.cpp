@@ -401,6 +401,27 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         }
         return (int)seen.size();
     };
+    // classes of the fields outside `mask` (mask fields zeroed); false past 32768 classes
+    auto build_classes = [&](uint32_t mask) {
+        table.clear();
+        ids.clear();
+        std::vector<double> r(CF_NPRIMARY);
+        for (int i = 0; i < NE; i++) {
+            prim(i, r);
+            for (int f = 0; f < CF_NPRIMARY; f++)
+                if (mask >> f & 1) r[f] = 0.;
+            std::string k((const char *)r.data(), r.size() * sizeof(double));
+            auto it = ids.find(k);
+            if (it == ids.end()) {
+                if ((int)table.size() >= 32768) return false;
+                it = ids.emplace(k, (int)table.size()).first;
+                table.push_back(r);
+            }
+            cls[i] = it->second;
+        }
+        return true;
+    };
+    const bool fits = build_classes(0);
     // Hybrid layout (per-element-calibrated models): when the full tuples exceed one workgroup's LDS table, stream up
     // to kHybMax fields per element (8 B each) and keep the rest in the LDS class table — the fields that split the
     // classes of the non-streamable fields the most first, among those the kernel reads directly (no host-derived
@@ -411,7 +432,7 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         const char *hy = getenv("SHUD_RHS_HYB");
         const uint32_t streamable = 1u << CF_macD | 1u << CF_macKsatH | 1u << CF_vAreaF | 1u << CF_KsatH |
                                     1u << CF_KsatV | 1u << CF_Sy | 1u << CF_RzD | 1u << CF_depression | 1u << CF_rough;
-        if (!h->lakeon && !(hy && hy[0] == '0') && count_tuples(0, kLdsClassMax) > kLdsClassMax &&
+        if (!h->lakeon && !(hy && hy[0] == '0') && (!fits || (int)table.size() > kLdsClassMax) &&
             count_tuples(streamable, kLdsClassMax) <= kLdsClassMax) {
             // base classes: the tuples of the fields that cannot be streamed; then, per streamable field, how many
             // (base class, value) pairs it makes — the fields that split the base classes most are streamed first
@@ -449,19 +470,10 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
             }
         }
     }
-    std::vector<double> r(CF_NPRIMARY);
-    for (int i = 0; i < NE; i++) {
-        prim(i, r);
-        for (int f = 0; f < CF_NPRIMARY; f++)
-            if (hmask >> f & 1) r[f] = 0.;
-        std::string k((const char *)r.data(), r.size() * sizeof(double));
-        auto it = ids.find(k);
-        if (it == ids.end()) {
-            if ((int)table.size() >= 32768) return 0;
-            it = ids.emplace(k, (int)table.size()).first;
-            table.push_back(r);
-        }
-        cls[i] = it->second;
+    if (hmask) {
+        if (!build_classes(hmask)) return 0;
+    } else if (!fits) {
+        return 0;
     }
     const int ncls = (int)table.size();
     // beyond what a 256-thread workgroup's LDS copy holds (128 classes) the class table goes to 1024-thread
