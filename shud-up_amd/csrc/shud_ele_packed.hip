@@ -160,9 +160,13 @@ __device__ __forceinline__ OwnRec load_own(const DevPacked &p, const YView &Y, i
 // before the caller's own-record loads, which they overlap), then stored; a longer table continues in a loop.
 // (A load -> wait -> ds_write per iteration cost one L2 round trip per 256 table words at every workgroup start.)
 constexpr int kTabBatch = 8;
+// SHUD_PT_NOCOPY (timing only, with SHUD_POWTAB=0): the pow tables are not copied (what the copy costs)
+#ifndef SHUD_PT_NOCOPY
+#define SHUD_PT_NOCOPY 0
+#endif
 template <int BS>
 __device__ __forceinline__ void tab_issue(const DevPacked &p, double (&tv)[kTabBatch]) {
-    const int nt = p.ntab;
+    const int nt = SHUD_PT_NOCOPY ? p.pt_off : p.ntab;
 #pragma unroll
     for (int k = 0; k < kTabBatch; k++) {
         const int t = (int)threadIdx.x + k * BS;
@@ -171,7 +175,7 @@ __device__ __forceinline__ void tab_issue(const DevPacked &p, double (&tv)[kTabB
 }
 template <int BS>
 __device__ __forceinline__ void tab_store(const DevPacked &p, const double (&tv)[kTabBatch], double *lct) {
-    const int nt = p.ntab;
+    const int nt = SHUD_PT_NOCOPY ? p.pt_off : p.ntab;
 #pragma unroll
     for (int k = 0; k < kTabBatch; k++) {
         const int t = (int)threadIdx.x + k * BS;
