@@ -82,8 +82,13 @@ inline bool cdiv_divisor_ok(double b) {
 #define SHUD_LDS_CLS_MAX 128
 #endif
 constexpr int kLdsClassMax = SHUD_LDS_CLS_MAX;
-// pow_tab's log + exp tables (shud_pow_tab.h: 256 x 4 + 128 x 2 doubles), staged in LDS after the class table
-constexpr int kPowTabDoubles = 4 * 256 + 2 * 128;
+// pow_tab's log + exp tables (shud_pow_tab.h: 256 x 4 + 128 x 2 doubles; SHUD_PT_COMPACT: 128 x 2.5 + 128 x 2), staged in
+// LDS after the class table (shud_rhs.cpp checks the sizes against the generated tables)
+#ifndef SHUD_PT_COMPACT
+#define SHUD_PT_COMPACT 0
+#endif
+constexpr int kPowTabLogDoubles = SHUD_PT_COMPACT ? 2 * 128 + 64 : 4 * 256;
+constexpr int kPowTabDoubles = kPowTabLogDoubles + 2 * 128;
 // most classes a 1024-thread workgroup stages in LDS ((560 x 33 + 1280) x 8 B = 154 KiB of the CU's 160 KiB: one
 // workgroup per CU, 4 waves/SIMD) — models with 129..560 distinct parameter tuples
 constexpr int kLdsClassMaxBig = 560;

@@ -441,7 +441,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
         else {   // satKfun, Equations.cpp:136-141
             // n/(n-1), (n-1)/n; pow_tab's tables from the workgroup's LDS copy (or the L2 class table's buffer)
             const double *pt = (LCT && SHUD_PT_LDS ? lct : p.ctab) + p.pt_off;
-            satkr = (SHUD_EABL & 16) ? satn : sat_kfun(satn, CL(ex1), CL(ex2), pt, pt + 4 * SHUD_PT_LOG_N);
+            satkr = (SHUD_EABL & 16) ? satn : sat_kfun(satn, CL(ex1), CL(ex2), pt, pt + kPowTabLogDoubles);
         }
     }
 

@@ -248,7 +248,7 @@ __device__ __forceinline__ double sat_kfun(double satn, double ex1, double ex2, 
     return SSQRT(satn) * tmp * tmp;
 }
 __device__ __forceinline__ double sat_kfun(double satn, double ex1, double ex2) {
-    return sat_kfun(satn, ex1, ex2, shud_pt_logtab, shud_pt_exptab);
+    return sat_kfun(satn, ex1, ex2, SHUD_PT_LOGTAB, shud_pt_exptab);
 }
 // SoilMoistureStress, is_sm_et.cpp:131-140 (truncated PI), with dth = ThetaS - ThetaR and
 // fcmr = ThetaS * 0.75 - ThetaR; b = (SatRatio * dth - ThetaR) / fcmr

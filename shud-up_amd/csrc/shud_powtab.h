@@ -39,24 +39,47 @@ SHUD_PT_FN void shud_pt_ld2(const double *p, double *a, double *b) {
     *a = v.x;
     *b = v.y;
 #else
-    *a = p[0];
-    *b = p[1];
+    __builtin_memcpy(a, p, 8);                    // (the tables may hold integer bit patterns: no aliasing of types)
+    __builtin_memcpy(b, p + 1, 8);
 #endif
 }
+SHUD_PT_FN float shud_pt_asf(uint32_t u) { float x; __builtin_memcpy(&x, &u, 4); return x; }
+
+// SHUD_PT_COMPACT: the 2.5-KiB log table (128 x {logc, logctail} + 128 float invc with 8 significant bits) and a
+// degree-10 log1p polynomial instead of the 8-KiB one (256 x 32 B) and degree 8 — a smaller LDS copy per workgroup
+#ifndef SHUD_PT_COMPACT
+#define SHUD_PT_COMPACT 0
+#endif
 
 // log x as hi + *tail (|tail| <= 2^-60 |hi| or so); ix = bits of x, x normal and positive; lt = the log table
 // (shud_pt_logtab or a copy of it)
 SHUD_PT_FN double shud_pt_log(uint64_t ix, double *tail, const double *lt) {
     const uint64_t tmp = ix - SHUD_PT_OFF;
+#if SHUD_PT_COMPACT
+    const int i = (int)((tmp >> 45) & 127);
+#else
     const int i = (int)((tmp >> 44) & 255);
+#endif
     const int64_t k = (int64_t)tmp >> 52;                    // arithmetic shift: the exponent relative to OFF
     const uint64_t iz = ix - (tmp & (0xfffULL << 52));
     const double z = shud_pt_asd(iz);
     const double kd = (double)k;
+#if SHUD_PT_COMPACT
+    double logc, logctail;
+    shud_pt_ld2(lt + 2 * i, &logc, &logctail);
+#ifdef __HIPCC__
+    const double invc = (double)((const float *)(lt + 2 * SHUD_PT_CLOG_N))[i];
+#else
+    float fi;
+    __builtin_memcpy(&fi, (const char *)(lt + 2 * SHUD_PT_CLOG_N) + 4 * i, 4);
+    const double invc = (double)fi;
+#endif
+#else
     double invc, logc;
     shud_pt_ld2(lt + 4 * i, &invc, &logc);
     const double logctail = lt[4 * i + 2];
-    const double r = __builtin_fma(z, invc, -1.0);           // exact: invc has 9 significant bits
+#endif
+    const double r = __builtin_fma(z, invc, -1.0);           // exact: invc has 9 (compact: 8) significant bits
     // k ln2 + log c + r, in double-double
     const double t1 = kd * SHUD_PT_LN2HI + logc;
     const double t2 = t1 + r;
@@ -76,7 +99,14 @@ SHUD_PT_FN double shud_pt_log(uint64_t ix, double *tail, const double *lt) {
     const double A4 = -0x1.5555555555555p-1;                 // -2/3
     const double A5 = -0x1.2492492492492p+0;                 // -8/7
     const double A6 = 1.0;
+#if SHUD_PT_COMPACT
+    // ... + r^9/9 - r^10/10 (|r| < 2^-8 + 2^-9: degree 8 would leave ~2^-62 |r|)
+    const double A7 = 0x1.c71c71c71c71cp+0;                  // 16/9
+    const double A8 = -0x1.999999999999ap+0;                 // -8/5
+    const double p = ar3 * (A1 + r * A2 + ar2 * (A3 + r * A4 + ar2 * (A5 + r * A6 + ar2 * (A7 + r * A8))));
+#else
     const double p = ar3 * (A1 + r * A2 + ar2 * (A3 + r * A4 + ar2 * (A5 + r * A6)));
+#endif
     const double lo = lo1 + lo2 + lo3 + lo4 + p;
     const double y = hi + lo;
     *tail = hi - y + lo;
@@ -140,4 +170,11 @@ SHUD_PT_FN double shud_pow_tab_t(double x, double y, const double *lt, const dou
     return shud_pt_exp(ehi, elo, et);
 }
 // with the tables in __constant__ memory (device) / static arrays (host)
-SHUD_PT_FN double shud_pow_tab(double x, double y) { return shud_pow_tab_t(x, y, shud_pt_logtab, shud_pt_exptab); }
+#if SHUD_PT_COMPACT
+#define SHUD_PT_LOGTAB ((const double *)shud_pt_clogtab)
+#define SHUD_PT_LOG_DOUBLES (2 * SHUD_PT_CLOG_N + SHUD_PT_CLOG_N / 2)
+#else
+#define SHUD_PT_LOGTAB shud_pt_logtab
+#define SHUD_PT_LOG_DOUBLES (4 * SHUD_PT_LOG_N)
+#endif
+SHUD_PT_FN double shud_pow_tab(double x, double y) { return shud_pow_tab_t(x, y, SHUD_PT_LOGTAB, shud_pt_exptab); }

@@ -517,9 +517,15 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     // pow_tab's tables (shud_pow_tab.h) after the class table, 16-B aligned: one buffer, one LDS copy per workgroup
     const int pt_off = ((int)ctab.size() + 1) & ~1;
     ctab.resize((size_t)pt_off + kPowTabDoubles, 0.0);
-    static_assert(kPowTabDoubles == 4 * SHUD_PT_LOG_N + 2 * SHUD_PT_EXP_N, "pow_tab table size");
+#if SHUD_PT_COMPACT
+    static_assert(sizeof shud_pt_clogtab == 8 * kPowTabLogDoubles, "pow_tab");
+    memcpy(&ctab[pt_off], shud_pt_clogtab, sizeof shud_pt_clogtab);
+#else
+    static_assert(kPowTabLogDoubles == 4 * SHUD_PT_LOG_N && sizeof shud_pt_logtab == 8 * kPowTabLogDoubles, "pow_tab");
     memcpy(&ctab[pt_off], shud_pt_logtab, sizeof shud_pt_logtab);
-    memcpy(&ctab[pt_off + 4 * SHUD_PT_LOG_N], shud_pt_exptab, sizeof shud_pt_exptab);
+#endif
+    static_assert(kPowTabDoubles == kPowTabLogDoubles + 2 * SHUD_PT_EXP_N, "pow_tab table size");
+    memcpy(&ctab[pt_off + kPowTabLogDoubles], shud_pt_exptab, sizeof shud_pt_exptab);
     std::vector<double2> zz(NE), ged(3 * (size_t)NE);
     std::vector<int4> meta(NE);
     std::vector<int> sfirst(NE);

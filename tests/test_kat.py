@@ -294,10 +294,12 @@ def _pow_tab_operands(n=1 << 20, seed=11):
     return np.concatenate([x, edge_x]), np.concatenate([y, edge_y])
 
 
-def _pow_tab_lib(tmp_path):
+def _pow_tab_lib(tmp_path, compact=None):
+    """the C build of shud_powtab.h (compact: force SHUD_PT_COMPACT; None: the header's default, as the kernels)"""
     import subprocess
-    so = str(tmp_path / "libpowtab.so")
-    subprocess.check_call(["gcc", "-O2", "-ffp-contract=off", "-fno-fast-math", "-shared", "-fPIC", "-I",
+    so = str(tmp_path / f"libpowtab{'' if compact is None else compact}.so")
+    flags = [] if compact is None else [f"-DSHUD_PT_COMPACT={compact}"]
+    subprocess.check_call(["gcc", "-O2", "-ffp-contract=off", "-fno-fast-math", "-shared", "-fPIC"] + flags + ["-I",
                            os.path.join(PKG_DIR, "csrc"), "-o", so,
                            os.path.join(os.path.dirname(__file__), "pow_tab_emul.c"), "-lm"])
     lib = C.CDLL(so)
@@ -306,13 +308,14 @@ def _pow_tab_lib(tmp_path):
     return lib
 
 
-def test_pow_tab_accuracy(tmp_path):
+@pytest.mark.parametrize("compact", [0, 1])
+def test_pow_tab_accuracy(tmp_path, compact):
     """pow_tab restated in C from the same header the kernels compile (glibc's correctly rounded fma): within 1 ulp
     of glibc's pow (the reference's libm) everywhere on satKfun's domain, bit-identical to it on >= 99.5 % of the
     operands, and within 0.7 ulp of the exact x^y (decimal, 50 digits) wherever the two differ (sampled) — glibc's
     pow is itself within ~0.51 ulp there."""
     from decimal import Decimal, getcontext
-    lib = _pow_tab_lib(tmp_path)
+    lib = _pow_tab_lib(tmp_path, compact)
     x, y = _pow_tab_operands()
     got, ref = np.zeros_like(x), np.zeros_like(x)
     lib.pow_tab_eval(x.ctypes.data, y.ctypes.data, x.size, got.ctypes.data)
