@@ -85,7 +85,7 @@ constexpr int kLdsClassMax = SHUD_LDS_CLS_MAX;
 // pow_tab's log + exp tables (shud_pow_tab.h: 256 x 4 + 128 x 2 doubles; SHUD_PT_COMPACT: 128 x 2.5 + 128 x 2), staged in
 // LDS after the class table (shud_rhs.cpp checks the sizes against the generated tables)
 #ifndef SHUD_PT_COMPACT
-#define SHUD_PT_COMPACT 0
+#define SHUD_PT_COMPACT 1
 #endif
 constexpr int kPowTabLogDoubles = SHUD_PT_COMPACT ? 2 * 128 + 64 : 4 * 256;
 constexpr int kPowTabDoubles = kPowTabLogDoubles + 2 * 128;

@@ -5,7 +5,7 @@
 //
 // Why: OCML's pow core (pow_pos) costs ~180 VALU per call — an extended-precision log built from ~60 dependent
 // two-sum steps and an extended exp — and satKfun's two calls were 314 of the element kernel's 1,409 VALU per wave
-// (profiles/r05/ele_attr).  Here the log is a 256-entry table + a degree-8 polynomial in double-double and the exp a
+// (profiles/r05/ele_attr).  Here the log is a table + a degree-8 (compact: 10) polynomial in double-double and the exp a
 // 128-entry table of 2^(i/128) + a degree-5 polynomial: ~60 VALU and 3 table loads per call, error within ~0.51 ulp
 // of the true x^y (tests/test_kat.py measures it), where glibc's pow (the reference's) is within ~0.52 ulp too and
 // OCML's within ~1 ulp.  The element kernel reads the tables from its LDS copy (the per-lane gathers from
@@ -45,10 +45,13 @@ SHUD_PT_FN void shud_pt_ld2(const double *p, double *a, double *b) {
 }
 SHUD_PT_FN float shud_pt_asf(uint32_t u) { float x; __builtin_memcpy(&x, &u, 4); return x; }
 
-// SHUD_PT_COMPACT: the 2.5-KiB log table (128 x {logc, logctail} + 128 float invc with 8 significant bits) and a
-// degree-10 log1p polynomial instead of the 8-KiB one (256 x 32 B) and degree 8 — a smaller LDS copy per workgroup
+// SHUD_PT_COMPACT (default): the 2.5-KiB log table (128 x {logc, logctail} + 128 float invc with 8 significant bits)
+// and a degree-10 log1p polynomial instead of the 8-KiB one (256 x 32 B) and degree 8.  The tables are copied into
+// every element workgroup's LDS, and that copy is not free: 10 KiB more per workgroup measured 3 % of the element
+// kernel (pow_pos with and without the unused copy, profiles/r05/pow_ab/abl_compact.log); compact vs full tables
+// 0.5768 vs 0.5902 ms per eval, the same accuracy (0.51 ulp, tests/test_kat.py).  0: the full tables (A/B).
 #ifndef SHUD_PT_COMPACT
-#define SHUD_PT_COMPACT 0
+#define SHUD_PT_COMPACT 1
 #endif
 
 // log x as hi + *tail (|tail| <= 2^-60 |hi| or so); ix = bits of x, x normal and positive; lt = the log table
