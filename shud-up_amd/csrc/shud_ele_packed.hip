@@ -159,7 +159,13 @@ __device__ __forceinline__ OwnRec load_own(const DevPacked &p, const YView &Y, i
 // class table global -> LDS by BS threads: the first kTabBatch loads of every thread are issued together (and
 // before the caller's own-record loads, which they overlap), then stored; a longer table continues in a loop.
 // (A load -> wait -> ds_write per iteration cost one L2 round trip per 256 table words at every workgroup start.)
-constexpr int kTabBatch = 8;
+// SHUD_TAB16 (default): 16-B loads and ds_write_b128 (the table is an even number of 16-B aligned words): half the
+// load / LDS-write instructions for the same bytes — the per-workgroup copy is a measurable share of the kernel
+// (10 KiB more of it cost 3 %, profiles/r05/pow_ab/abl_compact.log).  0: 8-B words (A/B).
+#ifndef SHUD_TAB16
+#define SHUD_TAB16 1
+#endif
+constexpr int kTabBatch = 8;                             // 8-B words per thread in the first batch
 // SHUD_PT_NOCOPY (timing only, with SHUD_POWTAB=0): the pow tables are not copied (what the copy costs)
 #ifndef SHUD_PT_NOCOPY
 #define SHUD_PT_NOCOPY 0
@@ -167,6 +173,17 @@ constexpr int kTabBatch = 8;
 template <int BS>
 __device__ __forceinline__ void tab_issue(const DevPacked &p, double (&tv)[kTabBatch]) {
     const int nt = SHUD_PT_NOCOPY ? p.pt_off : p.ntab;
+    if (SHUD_TAB16) {
+        const int nt2 = (nt + 1) >> 1;
+#pragma unroll
+        for (int k = 0; k < kTabBatch / 2; k++) {
+            const int t = (int)threadIdx.x + k * BS;
+            const double2 v = t < nt2 ? ((const double2 *)p.ctab)[t] : make_double2(0., 0.);
+            tv[2 * k] = v.x;
+            tv[2 * k + 1] = v.y;
+        }
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < kTabBatch; k++) {
         const int t = (int)threadIdx.x + k * BS;
@@ -176,6 +193,17 @@ __device__ __forceinline__ void tab_issue(const DevPacked &p, double (&tv)[kTabB
 template <int BS>
 __device__ __forceinline__ void tab_store(const DevPacked &p, const double (&tv)[kTabBatch], double *lct) {
     const int nt = SHUD_PT_NOCOPY ? p.pt_off : p.ntab;
+    if (SHUD_TAB16) {
+        const int nt2 = (nt + 1) >> 1;
+#pragma unroll
+        for (int k = 0; k < kTabBatch / 2; k++) {
+            const int t = (int)threadIdx.x + k * BS;
+            if (t < nt2) ((double2 *)lct)[t] = make_double2(tv[2 * k], tv[2 * k + 1]);
+        }
+        for (int t = (int)threadIdx.x + kTabBatch / 2 * BS; t < nt2; t += BS)
+            ((double2 *)lct)[t] = ((const double2 *)p.ctab)[t];
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < kTabBatch; k++) {
         const int t = (int)threadIdx.x + k * BS;
