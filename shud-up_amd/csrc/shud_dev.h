@@ -59,7 +59,7 @@ enum ClassField {
     CF_fcmr = CF_NPRIMARY,  // ThetaS * 0.75 - ThetaR
     CF_dTh,                 // ThetaS - ThetaR
     CF_ex1, CF_ex2,         // Beta / (Beta - 1),  (Beta - 1) / Beta
-    CF_vb, CF_pj,           // 1 - VegFrac,  1 - ImpAF
+    CF_pj,                  // 1 - ImpAF  (1 - VegFrac is one subtraction in the kernel: cheaper than its LDS copy)
     CF_omh,                 // 1 - hAreaF
     CF_kmax,                // infKsatV * (1 - hAreaF) + macKsatV * hAreaF
     CF_ekA, CF_ekB,         // infKsatV * (1 - hAreaF),  hAreaF * macKsatV
@@ -67,9 +67,23 @@ enum ClassField {
     CF_r_fcmr, CF_r_dTh, CF_r_infD, CF_r_Sy,
     CF_COUNT
 };
+// fields the packed kernel reads; hAreaF, macKsatV, Beta and ImpAF enter only through derived fields and are kept
+// out of the class record (every word of the record is copied into each workgroup's LDS: 3 % of the element
+// kernel per 10 KiB, profiles/r05/pow_ab)
+constexpr bool cf_stored(int f) { return f != CF_hAreaF && f != CF_macKsatV && f != CF_Beta && f != CF_ImpAF; }
+constexpr int cf_pos(int f) {
+    int q = 0;
+    for (int g = 0; g < f; g++) q += cf_stored(g) ? 1 : 0;
+    return cf_stored(f) ? q : -1;
+}
+template <int F> struct CfPos {
+    static_assert(F >= 0 && F < CF_COUNT && cf_stored(F), "field not in the class record");
+    static constexpr int v = cf_pos(F);
+};
+constexpr int CF_NSTORED = cf_pos(CF_COUNT - 1) + 1;
 // record stride of the class table (8-B words), odd: lanes reading one field of different classes from the
 // LDS copy land on different banks (an even stride of 32 put every class on one bank)
-constexpr int CF_STRIDE = CF_COUNT | 1;
+constexpr int CF_STRIDE = CF_NSTORED | 1;
 // divisors that cdiv (shud_physics.h) may take with a host reciprocal: 0, +-inf, NaN, or |b| in [kCdivBmin,
 // kCdivBmax] (the handle checks every such divisor at create and otherwise keeps the plain-division layout)
 constexpr double kCdivBmin = 0x1p-20, kCdivBmax = 0x1p20;
@@ -77,7 +91,7 @@ inline bool cdiv_divisor_ok(double b) {
     const double a = b < 0 ? -b : b;
     return b == 0. || !(a < 1e308) || (a >= kCdivBmin && a <= kCdivBmax);    // !(a < 1e308): inf or NaN
 }
-// most classes one workgroup stages in LDS (128 x 33 x 8 B = 33 KiB)
+// most classes one workgroup stages in LDS (128 x 27 x 8 B = 27 KiB)
 #ifndef SHUD_LDS_CLS_MAX
 #define SHUD_LDS_CLS_MAX 128
 #endif

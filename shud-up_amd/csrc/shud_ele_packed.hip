@@ -432,7 +432,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
         if (SHUD_REP1) rep |= (c) ? (uint32_t)(bit) : 0u;                                                   \
         else report_w(m.err, (c), (bit), (slot), i, (cnt));                                                 \
     } while (0)
-#define CL(f) (LCT ? lct[cid * CF_LDS_STRIDE + CF_##f] : p.ctab[cid * CF_STRIDE + CF_##f])
+#define CL(f) (LCT ? lct[cid * CF_LDS_STRIDE + CfPos<CF_##f>::v] : p.ctab[cid * CF_STRIDE + CfPos<CF_##f>::v])
 #define CDIV(a, F) CDIV_(a, CL(F), CL(r_##F))
     // HYB: CLH(f) for a field the hybrid layout may stream (uniform test of its slot), CDIV_SY: a / Sy with Sy
     // streamed takes the IEEE division (the class reciprocal would be another class's)
@@ -489,7 +489,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
                     dg.q_eta[i] = 0. + snp.y + 0.; }
     } else if (MODE == 0 && !(SHUD_EABL & 8)) {
         const double satn_prev = csv.x;
-        const double va = CL(VegFrac), vb = CL(vb), pj = CL(pj);
+        const double va = CL(VegFrac), vb = 1. - va, pj = CL(pj);   // vb as the host derived it
         const double pet = snp.y, ptr = stl.x;
         ibeta = soil_moisture_stress(CDIV(satn_prev * CL(dTh) - ThR, fcmr));   // fc = ThS * 0.75
         Es = rmin(rmax(0., usf), pet) * vb;
@@ -636,7 +636,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
 #endif
         double qsf = 0., qsb = 0.;
         const int cn = cf_class(ncf);
-#define CN(f) (LCT ? lct[cn * CF_LDS_STRIDE + CF_##f] : p.ctab[cn * CF_STRIDE + CF_##f])
+#define CN(f) (LCT ? lct[cn * CF_LDS_STRIDE + CfPos<CF_##f>::v] : p.ctab[cn * CF_STRIDE + CfPos<CF_##f>::v])
         double hvn[4] = {0., 0., 0., 0.};                 // HYB: the neighbour's streamed fields (if it reads any)
         if (HYB == 1 && !(SHUD_HYBABL & 1) && p.hnb) hvn[0] = p.hv[nc];
         else if (HYB == 2 && !(SHUD_HYBABL & 1) && p.hnb) hload(p, nc, hvn);

@@ -498,7 +498,6 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         // the packed kernel's satKfun uses pow_pos (positive bases, finite exponents: shud_physics.h);
         // any other Beta keeps the SoA layout, whose kernel calls the full pow
         if (!(t[CF_Beta] > 1.) || !std::isfinite(t[CF_ex1]) || !std::isfinite(t[CF_ex2])) return 0;
-        t[CF_vb] = 1. - t[CF_VegFrac];
         t[CF_pj] = 1. - t[CF_ImpAF];
         t[CF_omh] = 1. - t[CF_hAreaF];
         t[CF_kmax] = t[CF_infKsatV] * (1. - t[CF_hAreaF]) + t[CF_macKsatV] * t[CF_hAreaF];
@@ -512,7 +511,8 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         t[CF_r_dTh] = 1. / t[CF_dTh];
         t[CF_r_infD] = 1. / t[CF_infD];
         t[CF_r_Sy] = 1. / t[CF_Sy];
-        for (int f = 0; f < CF_COUNT; f++) ctab[(size_t)c * CF_STRIDE + f] = t[f];
+        for (int f = 0; f < CF_COUNT; f++)
+            if (cf_stored(f)) ctab[(size_t)c * CF_STRIDE + cf_pos(f)] = t[f];
     }
     // pow_tab's tables (shud_pow_tab.h) after the class table, 16-B aligned: one buffer, one LDS copy per workgroup
     const int pt_off = ((int)ctab.size() + 1) & ~1;
