@@ -129,8 +129,12 @@ constexpr int kEleBS = SHUD_ELE_BS;
 #define SHUD_PT_LDS 1
 #endif
 // One 256-element tile per workgroup.  (Persistent workgroups — one per resident slot looping over XCD-chunked
-// tiles, the class table copied to LDS once per workgroup — measured 0.735 vs 0.657 ms: the tile loop took the
-// kernel to 96 VGPRs with spills, profiles/r03/ab_persist/.)
+// tiles, the class table copied to LDS once per workgroup — measured 0.735 vs 0.657 ms in round 3: the tile loop
+// took the kernel to 96 VGPRs with spills, profiles/r03/ab_persist/.  Round 5 (SHUD_PERSIST below): the spills were
+// machine-LICM hoisting the polynomial constants out of the tile loop; with -mllvm -disable-machine-licm the loop
+// fits 82 VGPRs without spills, bit-identical, and is still slower: 0.682 / 0.671 ms at 5 / 6 waves per SIMD vs
+// 0.608 ms, profiles/r05/persist/.  Other workgroup sizes: 384 / 512 / 768 threads 0.672 / 0.615 / 0.666 ms,
+// profiles/r05/ele_bs/.)
 // the element's own records, loaded before the workgroup's class-table barrier so both round trips overlap
 struct OwnRec {
     int4 mt;
@@ -265,6 +269,63 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         __syncthreads();
     }
     if (act) ele_body<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH, HYB>(m, p, Y, dy, i, cur, dg, lk, lct, own);
+}
+
+// SHUD_PERSIST (A/B, slower: see above; build with -DSHUD_PERSIST_NOLAUNDER -mllvm -disable-machine-licm): persistent workgroups — one per resident slot (the occupancy the runtime reports x CUs), each
+// copying the class + pow tables into LDS ONCE and then looping over its XCD chunk's tiles (workgroup b on XCD b & 7
+// takes tiles (b >> 3), (b >> 3) + K, ... of chunk b & 7, K workgroups per XCD), then the QrivDown tiles.  The next
+// tile's own record is loaded right after the previous tile's body.
+#ifndef SHUD_PERSIST
+#define SHUD_PERSIST 0
+#endif
+#ifndef SHUD_PERSIST_WAVES
+#define SHUD_PERSIST_WAVES 5
+#endif
+struct PersistArgs {
+    DevMesh m;
+    DevPacked p;
+    YView Y;
+    double *dy;
+    DevDiag dg;
+    DevLake lk;
+    int i0, n_compute, cur, per8, nq_tiles;
+};
+// the kernel's one argument, re-read from the kernarg segment in every tile iteration: a loop-invariant argument the
+// compiler hoists out of the tile loop stays live in SGPRs across the whole body (spills: r03's persistent attempt)
+__device__ __forceinline__ const PersistArgs *persist_args() {
+    const PersistArgs *a = (const PersistArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+#ifndef SHUD_PERSIST_NOLAUNDER
+    asm volatile("" : "+s"(a));
+#endif
+    return a;
+}
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB = 0>
+__global__ void __launch_bounds__(kEleBS, SHUD_PERSIST_WAVES)
+shud_ele_kernel_persist(PersistArgs args) {
+    extern __shared__ double lct[];
+    const int b = (int)blockIdx.x, K = (int)gridDim.x >> 3;
+    const int x = b & 7;
+    const PersistArgs *a = persist_args();
+    if (LCT) {
+        double tv[kTabBatch];
+        tab_issue<kEleBS>(a->p, tv);
+        tab_store<kEleBS>(a->p, tv, lct);
+        __syncthreads();
+    }
+    for (int t = b >> 3; t < a->per8; t += K) {
+        a = persist_args();
+        const int i = a->i0 + (x * a->per8 + t) * kEleBS + (int)threadIdx.x;
+        if (i < a->n_compute) {
+            const OwnRec own = load_own<FU1, GH>(a->p, a->Y, i, a->cur);
+            ele_body<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH, HYB>(a->m, a->p, a->Y, a->dy, i, a->cur, a->dg, a->lk, lct, own);
+        }
+        a = persist_args();
+    }
+    a = persist_args();
+    for (int q = b; q < a->nq_tiles; q += (int)gridDim.x) {
+        const int r = q * kEleBS + (int)threadIdx.x;
+        if (r < a->p.nqd) qd_pre<MODE, false>(a->m, a->p, a->Y, r, 0, nullptr);
+    }
 }
 
 // 129..kLdsClassMaxBig classes: the same body with the class table in LDS, staged by 1024-thread workgroups (one
@@ -1096,6 +1157,22 @@ static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, doubl
     const int nbq = nq > 0 ? ((nq + kEleBS - 1) / kEleBS + 7) / 8 * 8 : 0;
     const int q0 = qd_start(nb, p.qd_pm);
     const size_t lds = LCT ? (size_t)p.ntab * sizeof(double) : 0;
+    if constexpr (SHUD_PERSIST != 0) {
+        auto *fn = shud_ele_kernel_persist<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH, HYB>;
+        static int slots = 0;                   // resident workgroups per XCD (per instantiation)
+        if (!slots) {
+            int dev = 0, ncu = 0, per_cu = 0;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)fn, kEleBS, lds);
+            slots = std::max(1, ncu * std::max(per_cu, 1) / 8);
+        }
+        const int g = 8 * std::min(slots, nb / 8);
+        const int nqt = nq > 0 ? (nq + kEleBS - 1) / kEleBS : 0;
+        const PersistArgs pa{m, p, Y, dy, dg, lk, i0, i1, cur, nb / 8, nqt};
+        hipLaunchKernelGGL(fn, dim3(g), dim3(kEleBS), lds, s, pa);
+        return;
+    }
     hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH, HYB>), dim3(nb + nbq), dim3(kEleBS),
                        lds, s,
                        m, p, Y, dy, i0, i1, cur, dg, lk, nb / 8, nbq, q0);

@@ -426,9 +426,11 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     // to kHybMax fields per element (8 B each) and keep the rest in the LDS class table — the fields that split the
     // classes of the non-streamable fields the most first, among those the kernel reads directly (no host-derived
     // class constant depends on them; Sy's reciprocal is replaced by the IEEE division, the same bits).
-    // SHUD_RHS_HYB=0: off (A/B).
+    // SHUD_RHS_HYB=0: off (A/B); =2: KsatH streamed even when the classes fit (timing the hybrid path on any model).
     uint32_t hmask = 0;
-    {
+    if (const char *hf = getenv("SHUD_RHS_HYB"); hf && hf[0] == '2' && !h->lakeon) {
+        hmask = 1u << CF_KsatH;
+    } else {
         const char *hy = getenv("SHUD_RHS_HYB");
         const uint32_t streamable = 1u << CF_macD | 1u << CF_macKsatH | 1u << CF_vAreaF | 1u << CF_KsatH |
                                     1u << CF_KsatV | 1u << CF_Sy | 1u << CF_RzD | 1u << CF_depression | 1u << CF_rough;

@@ -42,9 +42,10 @@ def lib_for(v):
     """the bound library a variant runs on: production, or an A/B build loaded RTLD_LOCAL beside it"""
     if not v.startswith("lib:"):
         return runtime.lib() if "prod" not in _libs else _libs["prod"]
-    if v not in _libs:
-        _libs[v] = abi.bind(C.CDLL(os.path.join(ROOT, "shud-up_amd", "build", "ab", f"libshud_rhs_{v[4:]}.so")))
-    return _libs[v]
+    name = v[4:].split("+", 1)[0]
+    if name not in _libs:
+        _libs[name] = abi.bind(C.CDLL(os.path.join(ROOT, "shud-up_amd", "build", "ab", f"libshud_rhs_{name}.so")))
+    return _libs[name]
 
 
 def env_for(v):
@@ -53,8 +54,10 @@ def env_for(v):
         e = {"SHUD_RHS_PACKED": "1", "SHUD_RHS_ELE_VARIANT": "0", "SHUD_RHS_SEG_ORDER": "element"}
         e.update(kv.split("=", 1) for kv in v[3:].split("+"))
         return e
-    if v.startswith("lib:"):
-        return {"SHUD_RHS_PACKED": "1", "SHUD_RHS_ELE_VARIANT": "0", "SHUD_RHS_SEG_ORDER": "element"}
+    if v.startswith("lib:"):     # lib:NAME[+NAME=VAL...]: an A/B library, optionally with run-time switches
+        e = {"SHUD_RHS_PACKED": "1", "SHUD_RHS_ELE_VARIANT": "0", "SHUD_RHS_SEG_ORDER": "element"}
+        e.update(kv.split("=", 1) for kv in v[4:].split("+")[1:])
+        return e
     if v.startswith("soa"):
         return {"SHUD_RHS_PACKED": "0", "SHUD_RHS_ELE_VARIANT": v[3:] or "0"}
     return {"SHUD_RHS_PACKED": "1", "SHUD_RHS_ELE_VARIANT": "0",
