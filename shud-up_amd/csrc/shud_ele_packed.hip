@@ -134,7 +134,10 @@ constexpr int kEleBS = SHUD_ELE_BS;
 // machine-LICM hoisting the polynomial constants out of the tile loop; with -mllvm -disable-machine-licm the loop
 // fits 82 VGPRs without spills, bit-identical, and is still slower: 0.682 / 0.671 ms at 5 / 6 waves per SIMD vs
 // 0.608 ms, profiles/r05/persist/.  Other workgroup sizes: 384 / 512 / 768 threads 0.672 / 0.615 / 0.666 ms,
-// profiles/r05/ele_bs/.)
+// profiles/r05/ele_bs/.  In-tile neighbours from LDS — each lane staging {z_surf, z_bottom, isf, uYgw, effKH,
+// roughness} after updateElement with a per-wave ready flag, edges to a same-tile neighbour reading them instead of
+// four gathers, two class lookups and eff_kh — bit-identical and neutral (0.605 vs 0.599 ms, wall 0.582 vs 0.583);
+// gathering the one out-of-tile neighbour before the loop took 94 VGPRs and was slower, profiles/r05/nb_lds/.)
 // the element's own records, loaded before the workgroup's class-table barrier so both round trips overlap
 struct OwnRec {
     int4 mt;
