@@ -110,6 +110,13 @@ constexpr int CF_LDS_STRIDE = CF_STRIDE;   // the HBM table's record layout, cop
 #define SHUD_ELE_BS 256
 #endif
 constexpr int kEleBS = SHUD_ELE_BS;
+// SHUD_TILES (A/B, slower): consecutive 256-element tiles per workgroup of the single-launch kernel, one class/pow
+// table copy for both.  2 tiles (straight-line; a tile loop spills): 83 VGPRs / 5 waves 0.628 ms, forced to 6 waves
+// (80 VGPRs) 0.606 vs 0.602 ms, wall per eval 0.590 vs 0.578 (profiles/r05/tiles2/)
+#ifndef SHUD_TILES
+#define SHUD_TILES 1
+#endif
+constexpr int kTiles = SHUD_TILES;
 // SHUD_EABL (timing-only ablation builds for the per-phase attribution, results are WRONG when != 0): bit 0 the
 // segment loop, 1 the neighbour eff_kh (KsatH instead), 2 the edge loop, 3 f_etFlux, 4 satKfun (satkr = satn),
 // 5 the report_w ballots, 6 infiltration + recharge
@@ -261,7 +268,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         if (r < p.nqd) qd_pre<MODE, false>(m, p, Y, r, 0, nullptr);
         return;
     }
-    const int i = i0 + tile_of(per8, eb) * kEleBS + (int)threadIdx.x;   // elements [i0, n_compute)
+    const int i = i0 + tile_of(per8, eb) * (kEleBS * kTiles) + (int)threadIdx.x;   // elements [i0, n_compute)
     const bool act = i < n_compute;
     double tv[kTabBatch];
     if (LCT) tab_issue<kEleBS>(p, tv);
@@ -271,7 +278,21 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         tab_store<kEleBS>(p, tv, lct);
         __syncthreads();
     }
-    if (act) ele_body<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH, HYB>(m, p, Y, dy, i, cur, dg, lk, lct, own);
+    if (kTiles <= 2) {                                     // straight-line second tile (a loop spills)
+        if (act) ele_body<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH, HYB>(m, p, Y, dy, i, cur, dg, lk, lct, own);
+        if (kTiles == 2 && i + kEleBS < n_compute) {
+            own = load_own<FU1, GH>(p, Y, i + kEleBS, cur);
+            ele_body<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH, HYB>(m, p, Y, dy, i + kEleBS, cur, dg, lk, lct, own);
+        }
+        return;
+    }
+#pragma unroll 1
+    for (int t = 0; t < kTiles; t++) {                     // SHUD_TILES > 1: the next tiles reuse the LDS tables
+        const int it = i + t * kEleBS;
+        if (it >= n_compute) break;
+        if (t) own = load_own<FU1, GH>(p, Y, it, cur);
+        ele_body<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH, HYB>(m, p, Y, dy, it, cur, dg, lk, lct, own);
+    }
 }
 
 // SHUD_PERSIST (A/B, slower: see above; build with -DSHUD_PERSIST_NOLAUNDER -mllvm -disable-machine-licm): persistent workgroups — one per resident slot (the occupancy the runtime reports x CUs), each
@@ -469,6 +490,29 @@ __device__ __forceinline__ void hload(const DevPacked &p, int i, double (&v)[4])
     }
 }
 
+// SHUD_EDGE_PF (A/B, slower): a neighbour's gathered inputs (zz, class word, surface and groundwater stages), loaded
+// one edge ahead of their use (1), or edge 0's before the segment loop (2): 92 / 94 VGPRs, 5 waves per SIMD, element
+// kernel 0.620 / 0.627 vs 0.600 ms (6 waves at 80 VGPRs); forced to 6 waves it spills (0.752).  Occupancy hides the
+// gathers' latency better than the extra loads in flight per wave (profiles/r05/edge_pf/).
+#ifndef SHUD_EDGE_PF
+#define SHUD_EDGE_PF 0
+#endif
+struct EdgeIn {
+    double2 nzz;
+    double nsf, ngw;
+    int ncf;
+};
+template <bool GH>
+__device__ __forceinline__ EdgeIn load_edge(const DevPacked &p, const YView &Y, int nc) {
+    const uint32_t n16 = (uint32_t)nc << 4, n8 = (uint32_t)nc << 3;
+    EdgeIn e;
+    e.nzz = *at(p.zz, n16);
+    e.ncf = *at((const int *)p.meta + 3, n16);
+    e.nsf = GH ? Y.sf(nc) : *at(Y.y, n8);
+    e.ngw = GH ? Y.gw(nc) : *at(Y.y + 2 * (size_t)Y.n_own, n8);
+    return e;
+}
+
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB>
 __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, const YView &Y, double *__restrict__ dy,
                                          int i, int cur, const DevDiag &dg, const DevLake &lk, const double *lct,
@@ -623,6 +667,10 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     const double dgw_head = q_rech - q_exfil;
     if (i < nown) __builtin_nontemporal_store(is_lake ? 0. : CDIV_SY(q_infil - q_rech - Eu - Tu), atw(dy + nown, o8));
 
+#if SHUD_EDGE_PF == 2
+    // edge 0's neighbour gathers issued before the segment loop (in flight across it)
+    EdgeIn ein = load_edge<GH>(p, Y, mt.x >= 0 ? mt.x : i);
+#endif
     // ---- own river segments (fun_Seg_surface / fun_Seg_sub) and Qe2r (PassValue) ----
     const double dep = CLH(depression), rgh = CLH(rough);
     double qe2r_surf = 0., qe2r_sub = 0.;
@@ -679,9 +727,27 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
 #if SHUD_AREA_EARLY
     const double area = ldnt(at(p.area, o8));          // in flight across the edge loop
 #endif
+    const int n_edges = (is_lake || (SHUD_EABL & 4)) ? 0 : 3;   // lake elements: fun_Ele_lakeHorizon, all zero
+#if SHUD_EDGE_PF == 1
+    // software-pipelined neighbour gathers: edge j+1's loads are issued at the top of edge j's iteration
+    EdgeIn ein;
+    if (n_edges) ein = load_edge<GH>(p, Y, mt.x >= 0 ? mt.x : i);
+#endif
 #pragma unroll 1
-    for (int j = 0; j < ((is_lake || (SHUD_EABL & 4)) ? 0 : 3); j++) {   // lake elements: fun_Ele_lakeHorizon, all zero
+    for (int j = 0; j < n_edges; j++) {
         const int nb = j == 0 ? mt.x : j == 1 ? mt.y : mt.z;
+#if SHUD_EDGE_PF
+        const EdgeIn cur_e = ein;
+        if (j < 2) {
+            const int nb1 = j == 0 ? mt.y : mt.z;
+            ein = load_edge<GH>(p, Y, nb1 >= 0 ? nb1 : i);
+        }
+        const double2 g = ldnt2(at(p.ged + (size_t)j * NEl, o16));
+        const double2 nzz = cur_e.nzz;
+        const int ncf = cur_e.ncf;
+        const double nsf_raw = cur_e.nsf, ngw_raw = cur_e.ngw;
+        const int nc = nb >= 0 ? nb : i;
+#else
         const int nc = nb >= 0 ? nb : i;                  // boundary edge: harmless in-bounds loads
         // (edge 0's loads issued right after the own record instead — held through the vertical physics — took
         // the kernel to 96 VGPRs with spills and measured 0.707 vs 0.617 ms, profiles/r03/ab_prologue/)
@@ -691,6 +757,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
         const int ncf = *at((const int *)p.meta + 3, n16);
         const double nsf_raw = GH ? Y.sf(nc) : *at(Y.y, n8);
         const double ngw_raw = GH ? Y.gw(nc) : *at(Y.y + 2 * (size_t)nown, n8);
+#endif
         const double B = g.x, d2n = g.y;
 #if SHUD_RCP & 2
         const double rd2n = ldnt(at(p.r_d2n + (size_t)j * NEl, o8));
@@ -1155,7 +1222,7 @@ static int qd_start(int nb, int pm) {
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB = 0>
 static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1, int cur,
                      const DevDiag &dg, const DevLake &lk, hipStream_t s, int nq = 0) {
-    int nb = (i1 - i0 + kEleBS - 1) / kEleBS;
+    int nb = (i1 - i0 + kEleBS * kTiles - 1) / (kEleBS * kTiles);
     nb = (nb + 7) / 8 * 8;                  // block_id<1> deals blocks to XCDs in contiguous chunks
     const int nbq = nq > 0 ? ((nq + kEleBS - 1) / kEleBS + 7) / 8 * 8 : 0;
     const int q0 = qd_start(nb, p.qd_pm);

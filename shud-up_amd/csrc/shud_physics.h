@@ -261,6 +261,22 @@ __device__ __forceinline__ double sat_kfun(double satn, double ex1, double ex2) 
 #ifndef SHUD_COS_SMALL
 #define SHUD_COS_SMALL 1
 #endif
+// fma(a, b, c) for a constant addend c: v_fma_f64 with c in an SGPR pair (one VALU + two SALU moves), where the
+// compiler's v_fmac_f64 form needs c in a VGPR pair (two v_mov_b32 + the fmac: three VALU).  Same operation, same
+// bits.  cos_small's nine constant-addend steps: -14 static VALU; element kernel 0.6017 vs 0.6012 ms, wall per eval
+// 0.578 vs 0.580 ms (within noise, profiles/r05/tiles2/).  SHUD_FMA_SC=0: __builtin_fma (A/B).
+#ifndef SHUD_FMA_SC
+#define SHUD_FMA_SC 1
+#endif
+__device__ __forceinline__ double fma_sc(double a, double b, double c) {
+#if SHUD_FMA_SC
+    double r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+    return r;
+#else
+    return __builtin_fma(a, b, c);
+#endif
+}
 // OCML's __ocmlpriv_trigredsmall_f64 + __ocmlpriv_sincosred2_f64 (ocml.bc, ROCm 7.2) restated operation for
 // operation (their results come back in registers; a call to the bitcode's struct-returning functions went through
 // scratch and cost the kernel 48 spill instructions)
@@ -284,15 +300,15 @@ __device__ __forceinline__ double cos_small(double x) {            // 0 <= x < 2
     const double wl = (1.0 - w) - h;
     const double x4 = x2 * x2;
     double pc = __builtin_fma(x2, -0x1.907db46cc5e42p-37, 0x1.1eeb69037ab78p-29);
-    pc = __builtin_fma(x2, pc, -0x1.27e4fa17f65f6p-22);
-    pc = __builtin_fma(x2, pc, 0x1.a01a019f4ec90p-16);
-    pc = __builtin_fma(x2, pc, -0x1.6c16c16c16967p-10);
-    pc = __builtin_fma(x2, pc, 0x1.5555555555555p-5);
+    pc = fma_sc(x2, pc, -0x1.27e4fa17f65f6p-22);
+    pc = fma_sc(x2, pc, 0x1.a01a019f4ec90p-16);
+    pc = fma_sc(x2, pc, -0x1.6c16c16c16967p-10);
+    pc = fma_sc(x2, pc, 0x1.5555555555555p-5);
     const double cs = w + __builtin_fma(x4, pc, __builtin_fma(hi, -lo, wl));
     double ps = __builtin_fma(x2, 0x1.5e0b2f9a43bb8p-33, -0x1.ae600b42fdfa7p-26);
-    ps = __builtin_fma(x2, ps, 0x1.71de3796cde01p-19);
-    ps = __builtin_fma(x2, ps, -0x1.a01a019e83e5cp-13);
-    ps = __builtin_fma(x2, ps, 0x1.1111111110bb3p-7);
+    ps = fma_sc(x2, ps, 0x1.71de3796cde01p-19);
+    ps = fma_sc(x2, ps, -0x1.a01a019e83e5cp-13);
+    ps = fma_sc(x2, ps, 0x1.1111111110bb3p-7);
     const double x3 = hi * -x2;
     double sn = __builtin_fma(x3, ps, lo * 0.5);
     sn = __builtin_fma(x2, sn, -lo);
