@@ -495,7 +495,7 @@ def main():
         def integrator():
             h.set_step_inputs()        # the state a fresh handle starts from (step inputs + carried state reset)
             h.eval_device(0.0, yp, dyp)
-            return ode_timing(h, y_glob, ms_eval, warm_steps=int(os.environ.get("SHUD_BENCH_ODE_WARM", "5")))
+            return ode_timing(h, y_glob, ms_eval, warm_steps=int(os.environ.get("SHUD_BENCH_ODE_WARM", "0")))
         side("integrator", integrator)
     if world == 1 and not args.no_many_class:
         h.close()                      # free the default handle's device memory first
@@ -586,7 +586,7 @@ def e2e_timing(n_ele, days=1.0):
     return res
 
 
-def ode_timing(h, y0, ms_eval, max_steps=40, budget_s=4.0, warm_steps=5):
+def ode_timing(h, y0, ms_eval, max_steps=40, budget_s=4.0, warm_steps=0):
     """The device integrator (shud_ode_solve, SURVEY §8f f2: CVODE BDF/Newton/SPGMR as SetCVODE configures it,
     ccw's cfg.para tolerances) on the same mesh and handle: internal steps (CV_ONE_STEP) from the bench state,
     y never leaving HBM.  rhs_share = RHS evaluations x the RHS time measured above / wall time: the rest is
@@ -594,9 +594,10 @@ def ode_timing(h, y0, ms_eval, max_steps=40, budget_s=4.0, warm_steps=5):
     from shud_rhs.runtime import OdeSolver
     ode = OdeSolver(h, 0.0, y0, 1e-4, 1e-4, 1e-2, 30.0)
     flag, _, _ = ode.solve(1e9, one_step=True, y_out=False)        # first step: setup outside the timing
-    # a few more untimed steps (~20 ms of GPU work): the solver's fresh vectors were allocated and the first step
-    # prepared with the GPU mostly idle, and its first ~20 ms of load run inside the clock ramp (the headline's
-    # 200 settle evals, the many-class section's warm-up)
+    # warm_steps (SHUD_BENCH_ODE_WARM, default 0) more untimed steps: not a clock effect here — 5 of them time steps
+    # 7-46 instead of 2-41, where the solver runs order 2 with 128 instead of 117 RHS evaluations and 211 instead of
+    # 201 host syncs per 40 steps (4.85 vs 4.39 ms per step on one box, profiles/r05/ode_warm/), so the default keeps
+    # the steps every earlier round timed
     for _ in range(warm_steps):
         if flag < 0:
             break
