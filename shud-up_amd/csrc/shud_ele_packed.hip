@@ -248,15 +248,28 @@ __device__ __forceinline__ int qd_split(int b, int nb_q, int q0, int *e) {
     return -1;
 }
 
-template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB = 0>
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB = 0, int LSP = 0>
 __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, const YView &Y, double *__restrict__ dy,
                                          int i, int cur, const DevDiag &dg, const DevLake &lk, const double *lct,
                                          const OwnRec &own);
+// SHUD_LSPILL (default 1): the values the DY tail needs from the vertical part (Es, Eg, Tg, the two DY heads and the
+// cf word) are parked in per-thread LDS slots across the segment and edge loops (ds_write / ds_read on the LDS
+// address space; a volatile generic pointer became flat loads with a wait each) instead of ~11 VGPRs: 80 -> 72 VGPRs,
+// 7 waves per SIMD without scratch spills, element kernel -0.9 / -1.1 % in two interleaved A/Bs, same bits
+// (profiles/r05/lsp/).  Forcing 7 waves without it spills 20 VGPRs to scratch: 0.788 vs 0.608 ms.  The slots add
+// 11 KiB of LDS per workgroup, so the handle takes this instantiation only while 7 workgroups still fit in a CU's
+// 160 KiB (kLspLdsMax: 23,296 B per workgroup, the runtime's occupancy answer on gfx950, tools/lds_occ.hip), i.e. up
+// to ~35 parameter classes, and never for the diagnostic, lake or hybrid instantiations.
+#ifndef SHUD_LSPILL
+#define SHUD_LSPILL 1
+#endif
+constexpr int kLspN = 5;
+constexpr size_t kLspLdsMax = 23296;
 
 // HYB: the hybrid layout (DevPacked::hv): the streamed class fields come from the element's (and its neighbours')
 // per-element record, the rest from the LDS class table; 1 = one streamed field (one 8-B value per element, held in
 // one register pair), 2 = two to four
-template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB = 0>
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB = 0, int LSPK = 0>
 __global__ void __launch_bounds__(kEleBS, SHUD_ELE_WAVES)
 shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int i0, int n_compute, int cur,
                        DevDiag dg, DevLake lk, int per8, int nb_q, int q0) {
@@ -279,7 +292,8 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         __syncthreads();
     }
     if (kTiles <= 2) {                                     // straight-line second tile (a loop spills)
-        if (act) ele_body<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH, HYB>(m, p, Y, dy, i, cur, dg, lk, lct, own);
+        if (act) ele_body<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH, HYB, LCT ? LSPK : 0>(m, p, Y, dy, i, cur, dg, lk, lct,
+                                                                                     own);
         if (kTiles == 2 && i + kEleBS < n_compute) {
             own = load_own<FU1, GH>(p, Y, i + kEleBS, cur);
             ele_body<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH, HYB>(m, p, Y, dy, i + kEleBS, cur, dg, lk, lct, own);
@@ -513,7 +527,7 @@ __device__ __forceinline__ EdgeIn load_edge(const DevPacked &p, const YView &Y, 
     return e;
 }
 
-template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB>
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB, int LSP>
 __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, const YView &Y, double *__restrict__ dy,
                                          int i, int cur, const DevDiag &dg, const DevLake &lk, const double *lct,
                                          const OwnRec &own) {
@@ -665,6 +679,14 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     // dgw = (recharge - exfil) - Qsub/area - Eg - Tg.  Ends the ET/vertical live ranges early.
     const double dsf_head = snp.x - q_infil + q_exfil;
     const double dgw_head = q_rech - q_exfil;
+    typedef __attribute__((address_space(3))) volatile double lds_vd;        // ds_write / ds_read, not flat
+    lds_vd *lsp = LSP ? (lds_vd *)(lct + p.ntab) + threadIdx.x : nullptr;
+    typedef __attribute__((address_space(3))) volatile int lds_vi;
+    lds_vi *lspi = LSP ? (lds_vi *)(lct + p.ntab + kLspN * kEleBS) + threadIdx.x : nullptr;   // + the cf word
+    if (LSP) {
+        lsp[0] = Es; lsp[kEleBS] = Eg; lsp[2 * kEleBS] = Tg; lsp[3 * kEleBS] = dsf_head; lsp[4 * kEleBS] = dgw_head;
+        lspi[0] = cf;
+    }
     if (i < nown) __builtin_nontemporal_store(is_lake ? 0. : CDIV_SY(q_infil - q_rech - Eu - Tu), atw(dy + nown, o8));
 
 #if SHUD_EDGE_PF == 2
@@ -862,15 +884,24 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
 #else
 #define AREA_DIV(a) SDIV(a, area)
 #endif
-    double dsf = dsf_head - AREA_DIV(sumsurf) - Es;
-    double dgw = dgw_head - AREA_DIV(sumsub) - Eg - Tg;
-    if (ibc > 0) dgw = 0;
-    else if (ibc < 0) dgw += AREA_DIV(m.eqbc[-ibc]);
+    double dsf, dgw;
+    if (LSP) {
+        const double es = lsp[0], eg = lsp[kEleBS], tg = lsp[2 * kEleBS], dsh = lsp[3 * kEleBS], dgh = lsp[4 * kEleBS];
+        dsf = dsh - AREA_DIV(sumsurf) - es;
+        dgw = dgh - AREA_DIV(sumsub) - eg - tg;
+    } else {
+        dsf = dsf_head - AREA_DIV(sumsurf) - Es;
+        dgw = dgw_head - AREA_DIV(sumsub) - Eg - Tg;
+    }
+    const int cf_t = LSP ? lspi[0] : cf;                      // (LSP: the cf word back from LDS)
+    const int ibc_t = LSP ? cf_ibc(cf_t) : ibc, iss_t = LSP ? cf_iss(cf_t) : iss;
+    if (ibc_t > 0) dgw = 0;
+    else if (ibc_t < 0) dgw += AREA_DIV(m.eqbc[-ibc_t]);
 #undef AREA_DIV
-    if (iss == 1) dsf += zero_over(area);                     // QSS is never assigned: 0.0 / area
-    else if (iss == 2) dgw += zero_over(area);
+    if (iss_t == 1) dsf += zero_over(area);                   // QSS is never assigned: 0.0 / area
+    else if (iss_t == 2) dgw += zero_over(area);
     dgw = CDIV_SY(dgw);
-    if (is_lake) { dsf = 0.; dgw = 0.; }                      // MD_f.cpp:146-150
+    if (LSP ? (LAKE && cf_t < 0) : is_lake) { dsf = 0.; dgw = 0.; }   // MD_f.cpp:146-150
 #undef CL
 #undef CLH
 #undef CDIV_SY
@@ -1219,14 +1250,19 @@ static int qd_start(int nb, int pm) {
     const long long q = (long long)nb * std::min(std::max(pm, 0), 1000) / 1000;
     return (int)(q / 8 * 8);
 }
-template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB = 0>
+// dynamic LDS of the 256-thread packed kernel: the class + pow tables, and with LSPK the parked DY-tail slots
+static size_t lds_bytes(const DevPacked &p, bool lct, bool lspk) {
+    if (!lct) return 0;
+    return (size_t)(p.ntab + (lspk ? kLspN * kEleBS : 0)) * sizeof(double) + (lspk ? kEleBS * sizeof(int) : 0);
+}
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB = 0, int LSPK = 0>
 static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1, int cur,
                      const DevDiag &dg, const DevLake &lk, hipStream_t s, int nq = 0) {
     int nb = (i1 - i0 + kEleBS * kTiles - 1) / (kEleBS * kTiles);
     nb = (nb + 7) / 8 * 8;                  // block_id<1> deals blocks to XCDs in contiguous chunks
     const int nbq = nq > 0 ? ((nq + kEleBS - 1) / kEleBS + 7) / 8 * 8 : 0;
     const int q0 = qd_start(nb, p.qd_pm);
-    const size_t lds = LCT ? (size_t)p.ntab * sizeof(double) : 0;
+    const size_t lds = lds_bytes(p, LCT, LSPK != 0);
     if constexpr (SHUD_PERSIST != 0) {
         auto *fn = shud_ele_kernel_persist<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH, HYB>;
         static int slots = 0;                   // resident workgroups per XCD (per instantiation)
@@ -1243,11 +1279,23 @@ static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, doubl
         hipLaunchKernelGGL(fn, dim3(g), dim3(kEleBS), lds, s, pa);
         return;
     }
-    hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH, HYB>), dim3(nb + nbq), dim3(kEleBS),
+    hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH, HYB, LSPK>), dim3(nb + nbq), dim3(kEleBS),
                        lds, s,
                        m, p, Y, dy, i0, i1, cur, dg, lk, nb / 8, nbq, q0);
 }
 
+// the plain LDS-table instantiation, with the DY-tail values parked in LDS when 7 workgroups still fit (SHUD_LSPILL)
+template <int MO, bool OP, bool DI, bool FU, bool GH>
+static void launch_plain(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1, int cur,
+                         const DevDiag &dg, const DevLake &lk, hipStream_t s, int nq) {
+    if constexpr (!DI && SHUD_LSPILL != 0) {
+        if (lds_bytes(p, true, true) <= kLspLdsMax) {
+            launch_p<MO, OP, DI, FU, true, false, GH, 0, 1>(m, p, Y, dy, i0, i1, cur, dg, lk, s, nq);
+            return;
+        }
+    }
+    launch_p<MO, OP, DI, FU, true, false, GH>(m, p, Y, dy, i0, i1, cur, dg, lk, s, nq);
+}
 bool launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1,
                                   int cur, int mode, bool open, bool diag, bool fu_unit, const DevDiag &dg,
                                   hipStream_t s, const DevLake *lake, bool interior, bool with_qd) {
@@ -1278,8 +1326,8 @@ bool launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YV
             else launch_p<MO, OP, DI, FU, true, false, false, 2>(m, p, Y, dy, i0, i1, cur, dg, lk, s, nq);   \
         }                                                                                                 \
         else if (p.ncls <= LDS_CLS_MAX) {                                                                 \
-            if (gh) launch_p<MO, OP, DI, FU, true, false, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s, nq); \
-            else launch_p<MO, OP, DI, FU, true, false, false>(m, p, Y, dy, i0, i1, cur, dg, lk, s, nq);   \
+            if (gh) launch_plain<MO, OP, DI, FU, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s, nq);          \
+            else launch_plain<MO, OP, DI, FU, false>(m, p, Y, dy, i0, i1, cur, dg, lk, s, nq);            \
         } else launch_p<MO, OP, DI, FU, false, false, true>(m, p, Y, dy, i0, i1, cur, dg, lk, s); } while (0)
 #define LFU(MO, OP, DI) do { if (fu_unit) LP(MO, OP, DI, true); else LP(MO, OP, DI, false); } while (0)
 #define LDI(MO, OP) do { if (diag) LFU(MO, OP, true); else LFU(MO, OP, false); } while (0)
