@@ -325,6 +325,18 @@ def test_many_classes(oracle_mod, monkeypatch, kind):
                           label=f"many-class {kind}", layout="soa" if kind == "soa" else "packed")
 
 
+@pytest.mark.parametrize("mode", [abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP])
+def test_mid_class_count(mode, oracle_mod):
+    """~66 parameter classes: the LDS class table without the DY-tail LDS slots (they fit beside tables of up to
+    ~35 classes only, shud_ele_packed.hip SHUD_LSPILL), against the oracle."""
+    m, y = cases.variant(20000, seed=23)
+    m.par["KsatH"] = m.par["KsatH"] * (1.0 + 1e-7 * (np.arange(m.num_ele) % 2))
+    lay = _runtime().RhsHandle(m, mode=mode).layout()
+    assert lay["packed"] and not lay.get("streamed_fields") and 40 <= lay["n_classes"] <= 128, lay
+    _compare_sequence(m, [y] + cases.states(m, None, 1, seed=5), mode, oracle_mod, ncalls=2, label="mid-class",
+                      layout="packed")
+
+
 def _hybrid_model(n=20000, seed=19):
     """every element its own KsatH, Rough, macD and Sy (four streamed fields, the 32-B per-element record)"""
     m, y = cases.variant(n, seed=seed)
