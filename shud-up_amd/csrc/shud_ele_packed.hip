@@ -409,7 +409,7 @@ __device__ __forceinline__ void halo_wait(const DevMesh &m, const HaloWait &hw, 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     report_w(m.err, late, 0x80u, 7, i);                      // SHUD_EF_HALO_WAIT
 }
-template <int MODE, bool OPEN, bool FU1>
+template <int MODE, bool OPEN, bool FU1, int LSPK = 0>
 __global__ void __launch_bounds__(256, SHUD_ELE_WAVES)
 shud_ele_kernel_packed_fold(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int n_int, int n_all, int cur,
                             DevDiag dg, int per8, int nb_int, HaloWait hw, int nb_q, int q0) {
@@ -431,7 +431,7 @@ shud_ele_kernel_packed_fold(DevMesh m, DevPacked p, YView Y, double *__restrict_
         if (act) own = load_own<FU1, false>(p, Y, i, cur);
         tab_store<256>(p, tv, lct);
         __syncthreads();
-        if (act) ele_body<MODE, OPEN, false, FU1, true, false, false>(m, p, Y, dy, i, cur, dg, lk, lct, own);
+        if (act) ele_body<MODE, OPEN, false, FU1, true, false, false, 0, LSPK>(m, p, Y, dy, i, cur, dg, lk, lct, own);
         return;
     }
     const int i = n_int + (b - nb_int) * 256 + (int)threadIdx.x;
@@ -443,7 +443,7 @@ shud_ele_kernel_packed_fold(DevMesh m, DevPacked p, YView Y, double *__restrict_
     if (act) own = load_own<FU1, true>(p, Y, i, cur);
     tab_store<256>(p, tv, lct);
     __syncthreads();
-    if (act) ele_body<MODE, OPEN, false, FU1, true, false, true>(m, p, Y, dy, i, cur, dg, lk, lct, own);
+    if (act) ele_body<MODE, OPEN, false, FU1, true, false, true, 0, LSPK>(m, p, Y, dy, i, cur, dg, lk, lct, own);
 }
 // Producer: the halo's bytes were written by earlier kernels of the comm stream (pack + RCCL, or the test's copy
 // kernel), complete before this one starts; the flag store follows an agent-scope release with an explicit
@@ -1351,9 +1351,16 @@ bool launch_element_kernel_packed_fold(const DevMesh &m, const DevPacked &p, con
     // QrivDown blocks among the interior tiles (they wait for the halo like the boundary ones: it has normally
     // arrived long before), pm of the interior blocks before them
     const int q0 = qd_start(nb_int, p.qd_pm_fold);
-    const size_t lds = (size_t)p.ntab * sizeof(double);
-#define LF(MO, OP, FU) hipLaunchKernelGGL((shud_ele_kernel_packed_fold<MO, OP, FU>), dim3(nb_int + nb_b + nbq), dim3(256), \
-                                          lds, s, m, p, Y, dy, n_int, n_all, cur, dg, nb_int / 8, nb_int, hw, nbq, q0)
+    // the DY-tail LDS slots as in the single launch (SHUD_LSPILL), while 7 workgroups still fit
+    const bool lsp = SHUD_LSPILL != 0 && lds_bytes(p, true, true) <= kLspLdsMax;
+    const size_t lds = lds_bytes(p, true, lsp);
+#define LF(MO, OP, FU) do {                                                                                        \
+        if (lsp) hipLaunchKernelGGL((shud_ele_kernel_packed_fold<MO, OP, FU, SHUD_LSPILL ? 1 : 0>),                \
+                                    dim3(nb_int + nb_b + nbq), dim3(256), lds, s, m, p, Y, dy, n_int, n_all, cur, dg, \
+                                    nb_int / 8, nb_int, hw, nbq, q0);                                              \
+        else hipLaunchKernelGGL((shud_ele_kernel_packed_fold<MO, OP, FU>), dim3(nb_int + nb_b + nbq), dim3(256),    \
+                                lds, s, m, p, Y, dy, n_int, n_all, cur, dg, nb_int / 8, nb_int, hw, nbq, q0);       \
+    } while (0)
     if (mode == 0) {
         if (open) { if (fu_unit) LF(0, true, true); else LF(0, true, false); }
         else { if (fu_unit) LF(0, false, true); else LF(0, false, false); }
