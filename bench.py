@@ -28,6 +28,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "shud-up_amd"))
 
 HBM_PEAK = 8.0e12          # B/s, MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+FP64_VALU_NOMINAL = 78.6e12   # FLOP/s, MI355X fp64 vector: 256 CUs x 64 fp64 FMA lanes x 2 FLOP x 2.4 GHz max clock
 METRIC = "element-flux-updates/sec (RHS evals × NumEle) at 1/2/4/8 GPUs; %HBM roofline"
 # algorithmic bytes per RHS (canonical): 392 B/element + 24 B/segment + 96 B/reach
 B_ELE, B_SEG, B_RIV = 392, 24, 96
@@ -293,6 +294,7 @@ def main():
     # GPU goes through in its first ~20 ms of load (element kernel 0.62 -> 0.74 -> 0.62 ms, profiles/r02/kt) then
     # falls outside the K timed evals instead of inside a short K = 20 window
     sp = stream_probe(local) if world == 1 else {}
+    vp = valu_probe(local) if world == 1 else {}
     hb("settle")
     ts = time.perf_counter()
     for _ in range(args.settle):
@@ -341,7 +343,11 @@ def main():
         timing_detail = {"source": "max over ranks of each rank's HIP-event span of the K evals on its compute stream",
                          "ms_per_step_events_max": float(tt[0]) / args.steps * 1e3,
                          "ms_per_step_rank_wall_max": float(tt[1]) / args.steps * 1e3,
-                         "ms_per_step_wall_incl_barrier": float(tt[2]) / args.steps * 1e3}
+                         "ms_per_step_wall_incl_barrier": float(tt[2]) / args.steps * 1e3,
+                         "value_wall_incl_barrier": NE * args.steps / float(tt[2]),
+                         "note": "value = NumEle x K / the slowest rank's event span (since round 5); rounds 1-4 "
+                                 "quoted the barrier-inclusive wall window (value_wall_incl_barrier), which also "
+                                 "holds the trailing barrier and the ranks' skew leaving it"}
         # the slowest rank's in-loop kernel times (each rank's HIP events on its own compute stream)
         kt = torch.tensor([ms_ele_loop, ms_riv_loop, ms_eval_loop], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(kt, op=dist.ReduceOp.MAX)
@@ -369,7 +375,11 @@ def main():
 
     # per-kernel times: HIP events recorded inside the timed loop on the handle's stream (= torch's current
     # stream); a partitioned handle also gets a serialized per-phase breakdown (halo exchange alone)
-    per = {"shud_ele_kernel": ms_ele_loop, "shud_riv_kernel": ms_riv_loop}
+    # river fold: the reaches ride in the element launch, so the "element kernel" events bracket the
+    # one launch that does both (shud_rhs_kernel_packed_rf) and the river slot reads ~0
+    folded = bool(h.layout().get("river_fold"))
+    per = ({"shud_rhs_kernel_rf": ms_ele_loop} if folded else
+           {"shud_ele_kernel": ms_ele_loop, "shud_riv_kernel": ms_riv_loop})
     ms_eval = ms_eval_loop
     if world > 1 and args.profile_reps > 0:
         _, per_ser = h.time_kernels(0.0, yp, dyp, args.profile_reps)
@@ -378,14 +388,15 @@ def main():
         dist.all_reduce(th, op=dist.ReduceOp.MAX)
         per["halo_exchange_serialized"] = float(th.item())
         dist.barrier()
-    ms_ele = per["shud_ele_kernel"]
-    ms_riv = per["shud_riv_kernel"]
+    ms_ele = per["shud_rhs_kernel_rf"] if folded else per["shud_ele_kernel"]
+    ms_riv = 0.0 if folded else per["shud_riv_kernel"]
     n_own_e = model.num_ele if world == 1 else part.n_own_ele
     n_own_r = model.num_riv if world == 1 else part.n_own_riv
     n_seg_local = model.num_seg
     ele_bytes = B_ELE * n_own_e + B_SEG * n_seg_local
     riv_bytes = B_RIV * n_own_r
-    achieved = ele_bytes / (ms_ele * 1e-3)
+    dom_bytes = ele_bytes + riv_bytes if folded else ele_bytes      # the dominant launch's algorithmic bytes
+    achieved = dom_bytes / (ms_ele * 1e-3)
 
     value = NE * args.steps / dt
     ms_step = dt / args.steps * 1e3
@@ -413,13 +424,14 @@ def main():
                    "y_ydot": "device-resident", "kernel_layout": h.layout()},
         "roofline": {
             "bound": "hbm",
-            "kernel": "shud_ele_kernel",
+            "kernel": ("shud_rhs_kernel_rf (elements + QrivDown pre-pass + reaches, one launch)" if folded
+                       else "shud_ele_kernel"),
             "achieved": achieved / 1e9,
             "peak": HBM_PEAK / 1e9,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK,
             "traffic": None,
-            "algorithmic_bytes_per_launch": ele_bytes,
+            "algorithmic_bytes_per_launch": dom_bytes,
             "kernel_ms": {k: v for k, v in per.items()},
             "kernel_ms_source": (f"HIP events around the kernels of {n_timed} of the {args.steps} timed evals "
                                  f"(1 in {t_stride}; handle stream)"),
@@ -445,8 +457,19 @@ def main():
     if sp:
         out["roofline"].update(sp)
         out["roofline"]["frac_of_stream_copy"] = achieved / 1e9 / sp["stream_copy_GBs"]
+    # what kind of box this line ran on: its HBM ceilings (STREAM) and its fp64 VALU rate + in-kernel clock under a
+    # dense fp64 load; the element kernel is co-limited by HBM and VALU issue (~0.67 of its cycles), so its time on a
+    # box whose VALU probe runs below nominal is also quoted scaled to the nominal rate
+    if sp or vp:
+        box = {k: sp[k] for k in ("stream_copy_GBs", "stream_read_GBs") if k in sp}
+        box.update(vp)
+        if vp.get("fp64_valu_TFLOPs"):
+            box["element_kernel_ms_box_normalized"] = ms_ele * vp["fp64_valu_TFLOPs"] * 1e12 / FP64_VALU_NOMINAL
+            box["element_kernel_ms_box_normalized_note"] = ("element kernel ms x (probe fp64 FMA rate / nominal "
+                                                            f"{FP64_VALU_NOMINAL / 1e12:g} TFLOP/s)")
+        out["box"] = box
     if world == 1:
-        tr = pmc_traffic(NE)
+        tr = pmc_traffic(NE, "shud_rhs_kernel_rf" if folded else "shud_ele_kernel")
         out["roofline"].update(tr)
         if out["roofline"].get("traffic"):
             out["roofline"]["frac_actual"] = out["roofline"]["traffic"] / (ms_ele * 1e-3) / HBM_PEAK
@@ -683,6 +706,40 @@ def stream_probe(dev, n=1 << 27, reps=20):
             "stream_copy_all_GBs": {names[k]: res[k] for k in (0, 1, 2)}, "stream_read_GBs": res[3]}
 
 
+def valu_probe(dev, blocks=2048, iters=4000, reps=5):
+    """fp64 VALU probe (shud-up_amd/libshud_stream.so shud_valu_probe): 8 independent fma chains per lane, 8 waves per
+    SIMD, non-trivial operands, HIP-event timed on torch's current stream, best of `reps` launches after 3 warm-ups;
+    and the in-kernel clock = s_memtime / s_memrealtime x 100 MHz stamped by every workgroup (median)."""
+    import ctypes
+    import torch
+    lib = ctypes.CDLL(os.path.join(ROOT, "shud-up_amd", "libshud_stream.so"))
+    lib.shud_valu_probe.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    sink = torch.zeros(256, dtype=torch.float64, device=f"cuda:{dev}")
+    stamps = torch.zeros(2 * blocks, dtype=torch.int64, device=f"cuda:{dev}")
+    st = torch.cuda.current_stream().cuda_stream
+    for _ in range(3):
+        if lib.shud_valu_probe(blocks, iters, sink.data_ptr(), stamps.data_ptr(), st) != 0:
+            return {}
+    best = None
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        lib.shud_valu_probe(blocks, iters, sink.data_ptr(), stamps.data_ptr(), st)
+        e1.record()
+        torch.cuda.synchronize()
+        sec = e0.elapsed_time(e1) * 1e-3
+        best = sec if best is None else min(best, sec)
+    st_h = stamps.cpu().numpy().reshape(-1, 2).astype(np.float64)
+    ok = st_h[:, 1] > 0
+    clock = float(np.median(st_h[ok, 0] / st_h[ok, 1])) * 0.1 if ok.any() else None     # GHz (100 MHz ticks)
+    flops = 2.0 * blocks * 256 * iters * 128
+    rate = flops / best
+    del sink, stamps
+    return {"fp64_valu_TFLOPs": rate / 1e12, "fp64_valu_frac_nominal": rate / FP64_VALU_NOMINAL,
+            "clock_GHz_in_kernel": clock, "valu_probe_ms": best * 1e3,
+            "valu_probe_note": "fp64 FMA chains, 8 waves/SIMD, best of 5 launches; clock = s_memtime / s_memrealtime"}
+
+
 def kernel_src_hash():
     """sha256 (16 hex) over the sources the RHS kernels are built from: keys profiles/pmc_summary.json so a
     PMC traffic figure is only reported for the kernel build it was measured on."""
@@ -699,7 +756,7 @@ def kernel_src_hash():
     return hh.hexdigest()[:16]
 
 
-def pmc_traffic(NE):
+def pmc_traffic(NE, kname="shud_ele_kernel"):
     """roofline.traffic from profiles/pmc_summary.json (rocprofv3 FETCH_SIZE / WRITE_SIZE passes, gfx950
     correction, tools/pmc_summary.py) when it was measured on this mesh AND this kernel build; else null."""
     pmc = os.path.join(ROOT, "profiles", "pmc_summary.json")
@@ -719,12 +776,12 @@ def pmc_traffic(NE):
                                f"{pj.get('kernel_src_hash')}): traffic not reported")
         return out
     k = pj.get("kernels", {})
-    if "shud_ele_kernel" in k:
-        out["traffic"] = k["shud_ele_kernel"]["hbm_bytes_per_launch"]
+    if kname in k:
+        out["traffic"] = k[kname]["hbm_bytes_per_launch"]
         out["traffic_source"] = ("profiles/pmc_summary.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE; per-pattern "
                                  "gfx950 calibration, profiles/r03/pmc_calib/)")
-        if "hbm_bytes_blanket_x2" in k["shud_ele_kernel"]:
-            out["traffic_blanket_x2"] = k["shud_ele_kernel"]["hbm_bytes_blanket_x2"]
+        if "hbm_bytes_blanket_x2" in k[kname]:
+            out["traffic_blanket_x2"] = k[kname]["hbm_bytes_blanket_x2"]
     if "shud_riv_kernel" in k:
         out["riv_traffic"] = k["shud_riv_kernel"]["hbm_bytes_per_launch"]
         if "hbm_bytes_blanket_x2" in k["shud_riv_kernel"]:

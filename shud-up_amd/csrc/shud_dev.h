@@ -92,10 +92,7 @@ inline bool cdiv_divisor_ok(double b) {
     return b == 0. || !(a < 1e308) || (a >= kCdivBmin && a <= kCdivBmax);    // !(a < 1e308): inf or NaN
 }
 // most classes one workgroup stages in LDS (128 x 27 x 8 B = 27 KiB)
-#ifndef SHUD_LDS_CLS_MAX
-#define SHUD_LDS_CLS_MAX 128
-#endif
-constexpr int kLdsClassMax = SHUD_LDS_CLS_MAX;
+constexpr int kLdsClassMax = 128;
 // pow_tab's log + exp tables (shud_pow_tab.h: 256 x 4 + 128 x 2 doubles; SHUD_PT_COMPACT: 128 x 2.5 + 128 x 2), staged in
 // LDS after the class table (shud_rhs.cpp checks the sizes against the generated tables)
 #ifndef SHUD_PT_COMPACT
@@ -129,14 +126,9 @@ struct DevPacked {
     int *seg_first;         // bits 0-30: first element-sorted segment of the element; bit 31: t_lai > ZERO
                             //   (f_etFlux's only use of LAI, MD_ET.cpp:381; rewritten with the step inputs)
     const double2 *sg_lc;   // [NS] element-sorted segments: {length, Cwr}
-    const double2 *sg_dk;   //   its reach's {depth, KsatH}
-    const int2 *sg_rb;      //   {reach, reach BC column}
-    const double *sg_bt;    //   its reach's BedThick
-    const int *sg_r;        // SHUD_SEG_RREC layout: [NS] the segment's (local) reach; with rrec [2 * local reaches]
+    const int *sg_r;        // [NS] the segment's (local) reach; with rrec [2 * local reaches]
     const double2 *rrec;    //   {depth, KsatH}, {BedThick, (BC column, 0) bits} per reach
-    double2 *qseg2;         // [NS] {QsegSurf, QsegSub}, written by the element kernel (element-sorted, or
-                            //   reach-sorted when seg_rpos is set)
-    const int *seg_rpos;    // nullptr, or element-sorted k -> reach-sorted slot (SHUD_RHS_SEG_ORDER=reach)
+    double2 *qseg2;         // [NS] {QsegSurf, QsegSub}, written by the element kernel (element-sorted)
     double2 *s_np;          // {net_prep, pot_evap}        step inputs (packed by shud_pack_step_kernel)
     double2 *s_tl;          // {pot_tran, ETP} (ETP: the eta > 2*ETP warning, MD_ET.cpp:391)
     double2 *s_fu;          // {fu_surf, fu_sub}            read only when not all ones
@@ -159,14 +151,35 @@ struct DevPacked {
     int qd_pm, qd_pm_fold;  // where the QrivDown blocks sit in the element launch: after this many permille of its
                             //   element blocks (single launch / folded partition launch; SHUD_QD_POS[_FOLD])
     int lds_big;            // 1: 129..kLdsClassMaxBig classes take the 1024-thread LDS-table kernel (host dispatch)
-    // correctly rounded reciprocals of static geometric divisors, uploaded only for a kernel built with the
-    // matching SHUD_RCP bit (shud_ele_rcp_mask()): 1 area, 2 Dist2Nabor [3][NE], 4 segment reach BedThick
-    const double *r_area, *r_d2n, *sg_rbt;
+    // river fold (unpartitioned, lake-free handles on the LDS class table): the reach tiles ride in the last blocks of
+    // the element launch and start once the element tiles and QrivDown blocks whose results they read have published
+    // them (shud_ele_packed.hip shud_rhs_kernel_packed_rf)
+    unsigned *rf_flag;      // [nb_e + nb_q] the eval's epoch once an element tile / QrivDown block's stores are out
+    const int *rf_tile;     // [rf_ntile] river block -> reach tile, in the order their inputs come due
+    const int4 *rf_dep;     // [rf_ntile] per reach tile {first, last element tile, first, last QrivDown block} it reads
+    int rf_ntile;           // reach tiles (256 reaches each); 0: no fold
+    int rf_qd_pm;           // where the QrivDown blocks sit in the folded launch (permille of the element blocks)
+    int rf_dbg_tile;        // test hook (shud_rhs_debug_rfold): this element tile spins rf_dbg_ticks before its work
+    unsigned long long rf_dbg_ticks;
 };
-// SHUD_RCP mask the packed element kernel was compiled with (shud_ele_packed.hip)
-int shud_ele_rcp_mask();
-// whether it reads the per-reach segment records (SHUD_SEG_RREC)
-int shud_ele_seg_rrec();
+// block geometry of the element launch (shared by the launcher and the host's river-fold dependency tables): nb_e element
+// blocks (256 elements each, padded to a multiple of 8 so the XCD chunks are whole), nb_q QrivDown blocks placed after
+// the first q0 element blocks
+struct EleGrid {
+    int nb_e, nb_q, q0;
+    int per8() const { return nb_e / 8; }
+    // launch block of element tile t (tile_of's inverse) and of QrivDown block qb
+    int block_of_tile(int t) const { const int eb = (t % per8()) * 8 + t / per8(); return eb < q0 ? eb : eb + nb_q; }
+    int block_of_qd(int qb) const { return q0 + qb; }
+};
+inline EleGrid ele_grid(int n, int nqd, int pm) {
+    EleGrid g;
+    g.nb_e = ((n + 255) / 256 + 7) / 8 * 8;
+    g.nb_q = nqd > 0 ? ((nqd + 255) / 256 + 7) / 8 * 8 : 0;
+    const int pc = pm < 0 ? 0 : pm > 1000 ? 1000 : pm;
+    g.q0 = (int)((long long)g.nb_e * pc / 1000 / 8 * 8);
+    return g;
+}
 
 struct DevDiag {                     // optional diagnostic outputs (ShudFluxOut), local numbering
     double *qele_surf, *qele_sub, *qele_surf_tot, *qele_sub_tot, *q_infil, *q_exfil, *q_recharge;
@@ -211,7 +224,7 @@ struct YView {
 };
 
 void launch_element_kernel(const DevMesh &m, const YView &Y, double *dy, int n_compute, int cur, int cur_e,
-                           int mode, bool open, bool diag, const DevDiag &dg, hipStream_t s, int variant = 0);
+                           int mode, bool open, bool diag, const DevDiag &dg, hipStream_t s);
 // with_qd: append the QrivDown workgroups (DevPacked::qdown) to this launch — only the last element launch of an
 // eval, which runs after the halo; returns whether they were appended (the river kernel then reads the slots)
 bool launch_element_kernel_packed(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1,
@@ -229,6 +242,12 @@ bool launch_element_kernel_packed_fold(const DevMesh &m, const DevPacked &p, con
                                        int n_all, int cur, int mode, bool open, bool fu_unit, const DevDiag &dg,
                                        const HaloWait &hw, hipStream_t s, bool with_qd = false);
 void launch_halo_flag(unsigned long long *flag, unsigned long long epoch, hipStream_t s);
+// river fold: the elements [0, n), the QrivDown pre-pass and the reaches in ONE launch (DevPacked::rf_*); epoch: this
+// eval's flag value (never 0); timeout: wall-clock ticks a reach tile polls before SHUD_EF_HALO_WAIT.  false: this
+// configuration has no folded instantiation (the caller launches the element and river kernels)
+bool launch_rhs_packed_rf(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int n, int cur, int mode,
+                          bool open, bool fu_unit, const DevDiag &dg, unsigned epoch, unsigned long long timeout,
+                          hipStream_t s);
 // test hooks (shud_rhs_debug_halo): a one-lane spin of `ticks` wall-clock ticks, and a plain vector copy (the
 // stand-in for RCCL's receive kernels writing the ghost buffers), both on the comm stream
 void launch_spin(unsigned long long ticks, hipStream_t s);

@@ -42,6 +42,18 @@ __device__ __forceinline__ void stnt2(double2 *p, double a, double b) {
     v.y = b;
     __builtin_nontemporal_store(v, (v2d *)p);
 }
+// one 16-byte write-through store (buffer_store_dwordx4 ... sc1): the line goes to memory at once and leaves this XCD's
+// L2, so a workgroup of the same launch on another XCD that reads it after the producer's flag sees the new bytes
+// (MI355X guide Guideline 16 R1: write-through payload, drained, then one flag store; no release fence).  off: bytes
+// from base, below 2 GiB (qseg2: 16 B x NS, NS < 2^27 by the handle's 32-bit stream offsets)
+__device__ __forceinline__ void st_wt16(double2 *base, uint32_t off, double a, double b) {
+    typedef unsigned v4u __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+    const unsigned long long ua = __builtin_bit_cast(unsigned long long, a), ub = __builtin_bit_cast(unsigned long long, b);
+    v4u v;
+    v.x = (unsigned)ua; v.y = (unsigned)(ua >> 32); v.z = (unsigned)ub; v.w = (unsigned)(ub >> 32);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)off, 0, 16);     // aux 16 = sc1
+}
 // element / segment streams are addressed as a wave-uniform base + a 32-bit byte offset, which the compiler
 // emits as global_load/store v, vOff, s[base] (saddr form): one 32-bit shift per record size shared by every
 // stream of that size, instead of a sign extension and a 64-bit address add per stream.  The handle keeps
@@ -51,23 +63,6 @@ __device__ __forceinline__ const T *at(const T *b, uint32_t off) { return (const
 template <class T>
 __device__ __forceinline__ T *atw(T *b, uint32_t off) { return (T *)((char *)b + off); }
 
-// SHUD_RCP (A/B of host reciprocals for static geometric divisors through cdiv; bit-identical either way):
-// bit 0 area (2 divisions per element + the eqbc term), bit 1 Dist2Nabor (2 per edge), bit 2 BedThick (1 per
-// segment).  Each costs 8 B of HBM per divisor instance and saves ~5 VALU per division.
-#ifndef SHUD_RCP
-#define SHUD_RCP 0
-#endif
-int shud_ele_rcp_mask() { return SHUD_RCP; }
-// SHUD_SEG_RREC (default): segments stream {length, Cwr} + a reach index and gather their reach's statics from one
-// 32-B per-reach record (−28 B of HBM per segment); 0: a 48-B segment record with the reach's statics copied into
-// it (A/B, rounds 1-3)
-#ifndef SHUD_SEG_RREC
-#define SHUD_SEG_RREC 1
-#endif
-int shud_ele_seg_rrec() { return SHUD_SEG_RREC; }
-#ifndef SHUD_AREA_EARLY
-#define SHUD_AREA_EARLY 1
-#endif
 // IEEE class tests (one v_cmp_class_f64 each): NaN | +-inf, and NaN | +-inf | negative (not -0.0)
 __device__ __forceinline__ bool nan_or_inf(double x) { return __builtin_isfpclass(x, 0x0003 | 0x0004 | 0x0200); }
 __device__ __forceinline__ bool bad_nonneg(double x) {
@@ -102,49 +97,24 @@ constexpr int CF_LDS_STRIDE = CF_STRIDE;   // the HBM table's record layout, cop
 // fun_Ele_lakeVertical / fun_Ele_lakeHorizon (Element.cpp:336-346, MD_ElementFlux.cpp:2-23) and get zero DY
 // (MD_f.cpp:146-150); bank edges of other elements exchange with the lake (MD_ElementFlux.cpp:46-53,107-121)
 // and leave their fluxes in DevLake for the lake kernel.  LAKE = false compiles all of it away.
-#ifndef SHUD_ELE_WAVES
-#define SHUD_ELE_WAVES 5        // min waves per SIMD: <= 96 VGPRs (rolled edge loop, no spills)
-#endif
-// elements per workgroup of the single-launch kernel (A/B: 512 / 1024 copy the LDS class table fewer times)
-#ifndef SHUD_ELE_BS
-#define SHUD_ELE_BS 256
-#endif
-constexpr int kEleBS = SHUD_ELE_BS;
-// SHUD_TILES (A/B, slower): consecutive 256-element tiles per workgroup of the single-launch kernel, one class/pow
-// table copy for both.  2 tiles (straight-line; a tile loop spills): 83 VGPRs / 5 waves 0.628 ms, forced to 6 waves
-// (80 VGPRs) 0.606 vs 0.602 ms, wall per eval 0.590 vs 0.578 (profiles/r05/tiles2/)
-#ifndef SHUD_TILES
-#define SHUD_TILES 1
-#endif
-constexpr int kTiles = SHUD_TILES;
-// SHUD_EABL (timing-only ablation builds for the per-phase attribution, results are WRONG when != 0): bit 0 the
-// segment loop, 1 the neighbour eff_kh (KsatH instead), 2 the edge loop, 3 f_etFlux, 4 satKfun (satkr = satn),
-// 5 the report_w ballots, 6 infiltration + recharge
-#ifndef SHUD_EABL
-#define SHUD_EABL 0
-#endif
-// SHUD_REP1 (default): f_etFlux's three conditions (negative flux, NaN, eta > 2 ETP) are collected in a lane bit mask
-// and reported together — one ballot per wave when none fired (the common case) instead of three; the same flags,
-// first indices and warning count (atomics commute).  (Deferring all five conditions to the end of the body kept the
-// mask live across the edge loop: 85 VGPRs, 5 waves/SIMD.)  0: report_w at each condition (A/B).
-#ifndef SHUD_REP1
-#define SHUD_REP1 1
-#endif
-// pow_tab's tables read from the workgroup's LDS copy (default) or gathered from the class-table buffer in HBM/L2
-// (SHUD_PT_LDS=0, A/B)
-#ifndef SHUD_PT_LDS
-#define SHUD_PT_LDS 1
-#endif
+constexpr int kEleWaves = 5;      // min waves per SIMD: <= 96 VGPRs (rolled edge loop, no spills)
+constexpr int kEleBS = 256;       // elements per workgroup
+// f_etFlux's three conditions (negative flux, NaN, eta > 2 ETP) are collected in a lane bit mask and reported together —
+// one ballot per wave when none fired (the common case) instead of three; the same flags, first indices and warning
+// count (atomics commute).  (Deferring all five conditions to the end of the body kept the mask live across the edge
+// loop: 85 VGPRs, 5 waves/SIMD.)
 // One 256-element tile per workgroup.  (Persistent workgroups — one per resident slot looping over XCD-chunked
 // tiles, the class table copied to LDS once per workgroup — measured 0.735 vs 0.657 ms in round 3: the tile loop
-// took the kernel to 96 VGPRs with spills, profiles/r03/ab_persist/.  Round 5 (SHUD_PERSIST below): the spills were
-// machine-LICM hoisting the polynomial constants out of the tile loop; with -mllvm -disable-machine-licm the loop
+// took the kernel to 96 VGPRs with spills, profiles/r03/ab_persist/.  Round 5 (a persistent kernel, commit a4b4e96):
+// the spills were machine-LICM hoisting the polynomial constants out of the tile loop; with -mllvm -disable-machine-licm the loop
 // fits 82 VGPRs without spills, bit-identical, and is still slower: 0.682 / 0.671 ms at 5 / 6 waves per SIMD vs
 // 0.608 ms, profiles/r05/persist/.  Other workgroup sizes: 384 / 512 / 768 threads 0.672 / 0.615 / 0.666 ms,
 // profiles/r05/ele_bs/.  In-tile neighbours from LDS — each lane staging {z_surf, z_bottom, isf, uYgw, effKH,
 // roughness} after updateElement with a per-wave ready flag, edges to a same-tile neighbour reading them instead of
 // four gathers, two class lookups and eff_kh — bit-identical and neutral (0.605 vs 0.599 ms, wall 0.582 vs 0.583);
-// gathering the one out-of-tile neighbour before the loop took 94 VGPRs and was slower, profiles/r05/nb_lds/.)
+// gathering the one out-of-tile neighbour before the loop took 94 VGPRs and was slower, profiles/r05/nb_lds/.  Two tiles
+// per workgroup sharing one table copy: 83 VGPRs / 5 waves 0.628 ms, forced to 6 waves 0.606 vs 0.602 ms,
+// profiles/r05/tiles2/.  Round-5 A/B switches that measured slower were removed in round 6; commit a4b4e96 holds them.)
 // the element's own records, loaded before the workgroup's class-table barrier so both round trips overlap
 struct OwnRec {
     int4 mt;
@@ -173,57 +143,31 @@ __device__ __forceinline__ OwnRec load_own(const DevPacked &p, const YView &Y, i
 // class table global -> LDS by BS threads: the first kTabBatch loads of every thread are issued together (and
 // before the caller's own-record loads, which they overlap), then stored; a longer table continues in a loop.
 // (A load -> wait -> ds_write per iteration cost one L2 round trip per 256 table words at every workgroup start.)
-// SHUD_TAB16 (default): 16-B loads and ds_write_b128 (the table is an even number of 16-B aligned words): half the
-// load / LDS-write instructions for the same bytes — the per-workgroup copy is a measurable share of the kernel
-// (10 KiB more of it cost 3 %, profiles/r05/pow_ab/abl_compact.log).  0: 8-B words (A/B).
-#ifndef SHUD_TAB16
-#define SHUD_TAB16 1
-#endif
+// The copy runs in 16-B words (global_load_dwordx4 / ds_write_b128; the table is an even number of 16-B aligned
+// words): half the load / LDS-write instructions of 8-B words for the same bytes — the per-workgroup copy is a
+// measurable share of the kernel (10 KiB more of it cost 3 %, profiles/r05/pow_ab/abl_compact.log).
 constexpr int kTabBatch = 8;                             // 8-B words per thread in the first batch
-// SHUD_PT_NOCOPY (timing only, with SHUD_POWTAB=0): the pow tables are not copied (what the copy costs)
-#ifndef SHUD_PT_NOCOPY
-#define SHUD_PT_NOCOPY 0
-#endif
 template <int BS>
 __device__ __forceinline__ void tab_issue(const DevPacked &p, double (&tv)[kTabBatch]) {
-    const int nt = SHUD_PT_NOCOPY ? p.pt_off : p.ntab;
-    if (SHUD_TAB16) {
-        const int nt2 = (nt + 1) >> 1;
+    const int nt2 = (p.ntab + 1) >> 1;
 #pragma unroll
-        for (int k = 0; k < kTabBatch / 2; k++) {
-            const int t = (int)threadIdx.x + k * BS;
-            const double2 v = t < nt2 ? ((const double2 *)p.ctab)[t] : make_double2(0., 0.);
-            tv[2 * k] = v.x;
-            tv[2 * k + 1] = v.y;
-        }
-        return;
-    }
-#pragma unroll
-    for (int k = 0; k < kTabBatch; k++) {
+    for (int k = 0; k < kTabBatch / 2; k++) {
         const int t = (int)threadIdx.x + k * BS;
-        tv[k] = t < nt ? p.ctab[t] : 0.;
+        const double2 v = t < nt2 ? ((const double2 *)p.ctab)[t] : make_double2(0., 0.);
+        tv[2 * k] = v.x;
+        tv[2 * k + 1] = v.y;
     }
 }
 template <int BS>
 __device__ __forceinline__ void tab_store(const DevPacked &p, const double (&tv)[kTabBatch], double *lct) {
-    const int nt = SHUD_PT_NOCOPY ? p.pt_off : p.ntab;
-    if (SHUD_TAB16) {
-        const int nt2 = (nt + 1) >> 1;
+    const int nt2 = (p.ntab + 1) >> 1;
 #pragma unroll
-        for (int k = 0; k < kTabBatch / 2; k++) {
-            const int t = (int)threadIdx.x + k * BS;
-            if (t < nt2) ((double2 *)lct)[t] = make_double2(tv[2 * k], tv[2 * k + 1]);
-        }
-        for (int t = (int)threadIdx.x + kTabBatch / 2 * BS; t < nt2; t += BS)
-            ((double2 *)lct)[t] = ((const double2 *)p.ctab)[t];
-        return;
-    }
-#pragma unroll
-    for (int k = 0; k < kTabBatch; k++) {
+    for (int k = 0; k < kTabBatch / 2; k++) {
         const int t = (int)threadIdx.x + k * BS;
-        if (t < nt) lct[t] = tv[k];
+        if (t < nt2) ((double2 *)lct)[t] = make_double2(tv[2 * k], tv[2 * k + 1]);
     }
-    for (int t = (int)threadIdx.x + kTabBatch * BS; t < nt; t += BS) lct[t] = p.ctab[t];
+    for (int t = (int)threadIdx.x + kTabBatch / 2 * BS; t < nt2; t += BS)
+        ((double2 *)lct)[t] = ((const double2 *)p.ctab)[t];
 }
 // workgroup -> tile: XCD-contiguous chunks (block_id<1>, shud_physics.h) with the chunk length per8 = grid/8
 // passed by the launcher, so no workgroup reads the grid size from the dispatch packet at its start
@@ -238,7 +182,7 @@ __device__ __forceinline__ int tile_of(int per8) { return tile_of(per8, (int)blo
 // kernel reads them, early enough that their dependent loads overlap element work instead of forming the launch's
 // tail.  q0 and nb_q are multiples of 8, so the element tiles keep their XCD chunks.
 struct HaloWait;
-template <int MODE, bool HALO>
+template <int MODE, bool HALO, bool WT = false>
 __device__ __forceinline__ void qd_pre(const DevMesh &m, const DevPacked &p, const YView &Y, int r, int n_int,
                                        const HaloWait *hw);
 // block b -> QrivDown block (>= 0, *e untouched) or -1 with *e = the element block ordinal
@@ -248,11 +192,12 @@ __device__ __forceinline__ int qd_split(int b, int nb_q, int q0, int *e) {
     return -1;
 }
 
-template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB = 0, int LSP = 0>
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB = 0, int LSP = 0,
+          bool WT = false>
 __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, const YView &Y, double *__restrict__ dy,
                                          int i, int cur, const DevDiag &dg, const DevLake &lk, const double *lct,
                                          const OwnRec &own);
-// SHUD_LSPILL (default 1): the values the DY tail needs from the vertical part (Es, Eg, Tg, the two DY heads and the
+// LSP: the values the DY tail needs from the vertical part (Es, Eg, Tg, the two DY heads and the
 // cf word) are parked in per-thread LDS slots across the segment and edge loops (ds_write / ds_read on the LDS
 // address space; a volatile generic pointer became flat loads with a wait each) instead of ~11 VGPRs: 80 -> 72 VGPRs,
 // 7 waves per SIMD without scratch spills, element kernel -0.9 / -1.1 % in two interleaved A/Bs, same bits
@@ -260,9 +205,6 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
 // 11 KiB of LDS per workgroup, so the handle takes this instantiation only while 7 workgroups still fit in a CU's
 // 160 KiB (kLspLdsMax: 23,296 B per workgroup, the runtime's occupancy answer on gfx950, tools/lds_occ.hip), i.e. up
 // to ~35 parameter classes, and never for the diagnostic, lake or hybrid instantiations.
-#ifndef SHUD_LSPILL
-#define SHUD_LSPILL 1
-#endif
 constexpr int kLspN = 5;
 constexpr size_t kLspLdsMax = 23296;
 
@@ -270,7 +212,7 @@ constexpr size_t kLspLdsMax = 23296;
 // per-element record, the rest from the LDS class table; 1 = one streamed field (one 8-B value per element, held in
 // one register pair), 2 = two to four
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB = 0, int LSPK = 0>
-__global__ void __launch_bounds__(kEleBS, SHUD_ELE_WAVES)
+__global__ void __launch_bounds__(kEleBS, kEleWaves)
 shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int i0, int n_compute, int cur,
                        DevDiag dg, DevLake lk, int per8, int nb_q, int q0) {
     extern __shared__ double lct[];                       // ntab doubles (class table + pow tables) when LCT
@@ -281,7 +223,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         if (r < p.nqd) qd_pre<MODE, false>(m, p, Y, r, 0, nullptr);
         return;
     }
-    const int i = i0 + tile_of(per8, eb) * (kEleBS * kTiles) + (int)threadIdx.x;   // elements [i0, n_compute)
+    const int i = i0 + tile_of(per8, eb) * kEleBS + (int)threadIdx.x;   // elements [i0, n_compute)
     const bool act = i < n_compute;
     double tv[kTabBatch];
     if (LCT) tab_issue<kEleBS>(p, tv);
@@ -291,79 +233,7 @@ shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         tab_store<kEleBS>(p, tv, lct);
         __syncthreads();
     }
-    if (kTiles <= 2) {                                     // straight-line second tile (a loop spills)
-        if (act) ele_body<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH, HYB, LCT ? LSPK : 0>(m, p, Y, dy, i, cur, dg, lk, lct,
-                                                                                     own);
-        if (kTiles == 2 && i + kEleBS < n_compute) {
-            own = load_own<FU1, GH>(p, Y, i + kEleBS, cur);
-            ele_body<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH, HYB>(m, p, Y, dy, i + kEleBS, cur, dg, lk, lct, own);
-        }
-        return;
-    }
-#pragma unroll 1
-    for (int t = 0; t < kTiles; t++) {                     // SHUD_TILES > 1: the next tiles reuse the LDS tables
-        const int it = i + t * kEleBS;
-        if (it >= n_compute) break;
-        if (t) own = load_own<FU1, GH>(p, Y, it, cur);
-        ele_body<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH, HYB>(m, p, Y, dy, it, cur, dg, lk, lct, own);
-    }
-}
-
-// SHUD_PERSIST (A/B, slower: see above; build with -DSHUD_PERSIST_NOLAUNDER -mllvm -disable-machine-licm): persistent workgroups — one per resident slot (the occupancy the runtime reports x CUs), each
-// copying the class + pow tables into LDS ONCE and then looping over its XCD chunk's tiles (workgroup b on XCD b & 7
-// takes tiles (b >> 3), (b >> 3) + K, ... of chunk b & 7, K workgroups per XCD), then the QrivDown tiles.  The next
-// tile's own record is loaded right after the previous tile's body.
-#ifndef SHUD_PERSIST
-#define SHUD_PERSIST 0
-#endif
-#ifndef SHUD_PERSIST_WAVES
-#define SHUD_PERSIST_WAVES 5
-#endif
-struct PersistArgs {
-    DevMesh m;
-    DevPacked p;
-    YView Y;
-    double *dy;
-    DevDiag dg;
-    DevLake lk;
-    int i0, n_compute, cur, per8, nq_tiles;
-};
-// the kernel's one argument, re-read from the kernarg segment in every tile iteration: a loop-invariant argument the
-// compiler hoists out of the tile loop stays live in SGPRs across the whole body (spills: r03's persistent attempt)
-__device__ __forceinline__ const PersistArgs *persist_args() {
-    const PersistArgs *a = (const PersistArgs *)__builtin_amdgcn_kernarg_segment_ptr();
-#ifndef SHUD_PERSIST_NOLAUNDER
-    asm volatile("" : "+s"(a));
-#endif
-    return a;
-}
-template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB = 0>
-__global__ void __launch_bounds__(kEleBS, SHUD_PERSIST_WAVES)
-shud_ele_kernel_persist(PersistArgs args) {
-    extern __shared__ double lct[];
-    const int b = (int)blockIdx.x, K = (int)gridDim.x >> 3;
-    const int x = b & 7;
-    const PersistArgs *a = persist_args();
-    if (LCT) {
-        double tv[kTabBatch];
-        tab_issue<kEleBS>(a->p, tv);
-        tab_store<kEleBS>(a->p, tv, lct);
-        __syncthreads();
-    }
-    for (int t = b >> 3; t < a->per8; t += K) {
-        a = persist_args();
-        const int i = a->i0 + (x * a->per8 + t) * kEleBS + (int)threadIdx.x;
-        if (i < a->n_compute) {
-            const OwnRec own = load_own<FU1, GH>(a->p, a->Y, i, a->cur);
-            ele_body<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH, HYB>(a->m, a->p, a->Y, a->dy, i, a->cur, a->dg, a->lk, lct, own);
-        }
-        a = persist_args();
-    }
-    a = persist_args();
-    for (int q = b; q < a->nq_tiles; q += (int)gridDim.x) {
-        const int r = q * kEleBS + (int)threadIdx.x;
-        if (r < a->p.nqd) qd_pre<MODE, false>(a->m, a->p, a->Y, r, 0, nullptr);
-    }
+    if (act) ele_body<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH, HYB, LCT ? LSPK : 0>(m, p, Y, dy, i, cur, dg, lk, lct, own);
 }
 
 // 129..kLdsClassMaxBig classes: the same body with the class table in LDS, staged by 1024-thread workgroups (one
@@ -410,7 +280,7 @@ __device__ __forceinline__ void halo_wait(const DevMesh &m, const HaloWait &hw, 
     report_w(m.err, late, 0x80u, 7, i);                      // SHUD_EF_HALO_WAIT
 }
 template <int MODE, bool OPEN, bool FU1, int LSPK = 0>
-__global__ void __launch_bounds__(256, SHUD_ELE_WAVES)
+__global__ void __launch_bounds__(256, kEleWaves)
 shud_ele_kernel_packed_fold(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int n_int, int n_all, int cur,
                             DevDiag dg, int per8, int nb_int, HaloWait hw, int nb_q, int q0) {
     extern __shared__ double lct[];
@@ -467,25 +337,8 @@ __global__ void shud_copy_f64_kernel(double *__restrict__ dst, const double *__r
         dst[k] = src[k];
 }
 
-// the streamed value of field slot k (1-based, wave-uniform) from a per-element record of up to 4 doubles, or the
-// class-table value c when the field is not streamed (k = 0).  SHUD_HYBSEL=0 (default): a uniform branch per read;
-// 1: both operands formed and a select chain on the uniform slot (fewer basic blocks, more VALU: measured slower,
-// profiles/r05/hybrid/).  SHUD_HYBABL (timing only): bit 0 the neighbours' streamed values, bit 1 the element's own,
-// replaced by the class-table value.
-#ifndef SHUD_HYBSEL
-#define SHUD_HYBSEL 0
-#endif
-#ifndef SHUD_HYBABL
-#define SHUD_HYBABL 0
-#endif
-__device__ __forceinline__ double hpick(const double (&v)[4], int k, double c) {
-    double r = c;
-    r = k == 1 ? v[0] : r;
-    r = k == 2 ? v[1] : r;
-    r = k == 3 ? v[2] : r;
-    r = k == 4 ? v[3] : r;
-    return r;
-}
+// the streamed value of field slot k (1-based, wave-uniform) from a per-element record of up to 4 doubles: a uniform
+// branch per read (a branch-free select chain on the uniform slot measured slower, profiles/r05/hybrid/)
 __device__ __forceinline__ double hsel(const double (&v)[4], int k) {
     return k == 1 ? v[0] : k == 2 ? v[1] : k == 3 ? v[2] : v[3];
 }
@@ -504,30 +357,10 @@ __device__ __forceinline__ void hload(const DevPacked &p, int i, double (&v)[4])
     }
 }
 
-// SHUD_EDGE_PF (A/B, slower): a neighbour's gathered inputs (zz, class word, surface and groundwater stages), loaded
-// one edge ahead of their use (1), or edge 0's before the segment loop (2): 92 / 94 VGPRs, 5 waves per SIMD, element
-// kernel 0.620 / 0.627 vs 0.600 ms (6 waves at 80 VGPRs); forced to 6 waves it spills (0.752).  Occupancy hides the
-// gathers' latency better than the extra loads in flight per wave (profiles/r05/edge_pf/).
-#ifndef SHUD_EDGE_PF
-#define SHUD_EDGE_PF 0
-#endif
-struct EdgeIn {
-    double2 nzz;
-    double nsf, ngw;
-    int ncf;
-};
-template <bool GH>
-__device__ __forceinline__ EdgeIn load_edge(const DevPacked &p, const YView &Y, int nc) {
-    const uint32_t n16 = (uint32_t)nc << 4, n8 = (uint32_t)nc << 3;
-    EdgeIn e;
-    e.nzz = *at(p.zz, n16);
-    e.ncf = *at((const int *)p.meta + 3, n16);
-    e.nsf = GH ? Y.sf(nc) : *at(Y.y, n8);
-    e.ngw = GH ? Y.gw(nc) : *at(Y.y + 2 * (size_t)Y.n_own, n8);
-    return e;
-}
-
-template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB, int LSP>
+// (Edge j+1's neighbour gathers issued at the top of edge j's iteration, or edge 0's before the segment loop: 92 / 94
+// VGPRs, 5 waves per SIMD, element kernel 0.620 / 0.627 vs 0.600 ms; forced to 6 waves it spills (0.752).  Occupancy
+// hides the gathers' latency better than the extra loads in flight per wave, profiles/r05/edge_pf/.)
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB, int LSP, bool WT>
 __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, const YView &Y, double *__restrict__ dy,
                                          int i, int cur, const DevDiag &dg, const DevLake &lk, const double *lct,
                                          const OwnRec &own) {
@@ -547,26 +380,18 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     const double etp = stl.y;
     const double2 fu = own.fu;
     const double2 csv = own.csv;
-    // REPORT: an error / warning condition, reported now; REPORT_ET: one of f_etFlux's, collected (SHUD_REP1)
-#define REPORT(c, bit, slot, cnt) do { if (!(SHUD_EABL & 32)) report_w(m.err, (c), (bit), (slot), i, (cnt)); } while (0)
-#define REPORT_ET(c, bit, slot, cnt) do {                                                                       \
-        if (SHUD_EABL & 32) break;                                                                          \
-        if (SHUD_REP1) rep |= (c) ? (uint32_t)(bit) : 0u;                                                   \
-        else report_w(m.err, (c), (bit), (slot), i, (cnt));                                                 \
-    } while (0)
+    // REPORT: an error / warning condition, reported now; REPORT_ET: one of f_etFlux's, collected in `rep`
+#define REPORT(c, bit, slot, cnt) report_w(m.err, (c), (bit), (slot), i, (cnt))
+#define REPORT_ET(c, bit) (rep |= (c) ? (uint32_t)(bit) : 0u)
 #define CL(f) (LCT ? lct[cid * CF_LDS_STRIDE + CfPos<CF_##f>::v] : p.ctab[cid * CF_STRIDE + CfPos<CF_##f>::v])
-#define CDIV(a, F) CDIV_(a, CL(F), CL(r_##F))
+#define CDIV(a, F) cdiv(a, CL(F), CL(r_##F))
     // HYB: CLH(f) for a field the hybrid layout may stream (uniform test of its slot), CDIV_SY: a / Sy with Sy
     // streamed takes the IEEE division (the class reciprocal would be another class's)
     double hvo[4] = {0., 0., 0., 0.};
-    if (HYB == 1 && !(SHUD_HYBABL & 2)) hvo[0] = p.hv[i];
-    else if (HYB == 2 && !(SHUD_HYBABL & 2)) hload(p, i, hvo);
-#if SHUD_HYBSEL
-#define CLH(f) ((HYB && !(SHUD_HYBABL & 2)) ? hpick(hvo, p.hslot1[CF_##f], CL(f)) : CL(f))
-#else
-#define CLH(f) ((HYB && !(SHUD_HYBABL & 2) && p.hslot1[CF_##f]) ? (HYB == 1 ? hvo[0] : hsel(hvo, p.hslot1[CF_##f])) : CL(f))
-#endif
-#define CDIV_SY(a) ((HYB && p.hslot1[CF_Sy]) ? SDIV(a, HYB == 1 ? hvo[0] : hsel(hvo, p.hslot1[CF_Sy])) : CDIV(a, Sy))
+    if (HYB == 1) hvo[0] = p.hv[i];
+    else if (HYB == 2) hload(p, i, hvo);
+#define CLH(f) ((HYB && p.hslot1[CF_##f]) ? (HYB == 1 ? hvo[0] : hsel(hvo, p.hslot1[CF_##f])) : CL(f))
+#define CDIV_SY(a) ((HYB && p.hslot1[CF_Sy]) ? (a) / (HYB == 1 ? hvo[0] : hsel(hvo, p.hslot1[CF_Sy])) : CDIV(a, Sy))
 
     // ---- f_update ----
     double usf = ysf_raw, uus = yus_raw;
@@ -585,13 +410,13 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
         deficit = aq - ugw;
         const double ThS = CL(ThetaS), ThR = CL(ThetaR);
         if (deficit <= 0.) { deficit = 0.; satn = 1.; theta = ThS; }
-        else { theta = SDIV(uus, deficit) * ThS; satn = CDIV(theta - ThR, dTh); }
+        else { theta = uus / deficit * ThS; satn = CDIV(theta - ThR, dTh); }
         if (satn > 0.99) { satn = 1.0; satkr = 1.0; theta = ThS; }
         else if (satn <= K_ZERO) { satn = 0.; satkr = 0.; theta = ThR; }
         else {   // satKfun, Equations.cpp:136-141
             // n/(n-1), (n-1)/n; pow_tab's tables from the workgroup's LDS copy (or the L2 class table's buffer)
-            const double *pt = (LCT && SHUD_PT_LDS ? lct : p.ctab) + p.pt_off;
-            satkr = (SHUD_EABL & 16) ? satn : sat_kfun(satn, CL(ex1), CL(ex2), pt, pt + kPowTabLogDoubles);
+            const double *pt = (LCT ? lct : p.ctab) + p.pt_off;
+            satkr = sat_kfun(satn, CL(ex1), CL(ex2), pt, pt + kPowTabLogDoubles);
         }
     }
 
@@ -609,7 +434,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
         eic = 0.;                                 // fun_Ele_lakeVertical: qEleE_IC = 0 (carried)
         if (DIAG) { dg.q_es[i] = 0.; dg.q_eu[i] = 0.; dg.q_eg[i] = 0.; dg.q_tu[i] = 0.; dg.q_tg[i] = 0.;
                     dg.q_eta[i] = 0. + snp.y + 0.; }
-    } else if (MODE == 0 && !(SHUD_EABL & 8)) {
+    } else if (MODE == 0) {
         const double satn_prev = csv.x;
         const double va = CL(VegFrac), vb = 1. - va, pj = CL(pj);   // vb as the host derived it
         const double pet = snp.y, ptr = stl.x;
@@ -626,14 +451,14 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
         } else { Tg = Tu = eic = 0.; }
         const double trans = Tg + Tu, evapo = Eu + Eg + Es, eta = eic + evapo + trans;
         uint32_t rep = 0;
-        REPORT_ET(eta > etp * 2., 0x10u, 4, true);        // printf warning, MD_ET.cpp:391-393
+        REPORT_ET(eta > etp * 2., 0x10u);        // printf warning, MD_ET.cpp:391-393
         // CheckNonNegative (functions.cpp:148-154): x < 0 || isnan || isinf || |x - NA| < ZERO is exactly
         // "NaN, an infinity, or a negative normal/subnormal" (-0.0 passes; x ~ -9999 is negative): one
         // v_cmp_class per value
         const bool neg = bad_nonneg(Es) || bad_nonneg(Eu) || bad_nonneg(Eg) || bad_nonneg(Tu) || bad_nonneg(Tg);
-        REPORT_ET(neg, 0x04u, 2, false);
-        REPORT_ET(!neg && (nan_or_inf(eta) || nan_or_inf(evapo) || nan_or_inf(trans)), 0x08u, 3, false);
-        if (SHUD_REP1 && __builtin_amdgcn_ballot_w64(rep != 0)) {
+        REPORT_ET(neg, 0x04u);
+        REPORT_ET(!neg && (nan_or_inf(eta) || nan_or_inf(evapo) || nan_or_inf(trans)), 0x08u);
+        if (__builtin_amdgcn_ballot_w64(rep != 0)) {
             report_w(m.err, rep & 0x04u, 0x04u, 2, i);
             report_w(m.err, rep & 0x08u, 0x08u, 3, i);
             report_w(m.err, rep & 0x10u, 0x10u, 4, i, true);
@@ -645,11 +470,11 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
 
     // ---- Flux_Infiltration (Element.cpp:271-303) and Flux_Recharge (:304-335); zero on lake elements ----
     double qi = 0., qex = 0., qr = 0.;
-    if (!is_lake && !(SHUD_EABL & 64)) {
+    if (!is_lake) {
         const double kmax = CL(kmax);
         const double av = usf + snp.x;
         if (ugw + uus > aq || deficit < uus) {
-            qex = SDIV(fabs(ugw + uus - aq), aq) * kmax;
+            qex = fabs(ugw + uus - aq) / aq * kmax;
         } else if (av > 0. && deficit > infD) {
             const double grad = 1. + CDIV(av, infD);
             double ek;
@@ -667,7 +492,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
             }
             if (!(infK <= 0. || KV <= 0.)) {
                 const double ku = infK * satkr;
-                qr = grad * SDIV((ku * KV) * (deficit + ugw), deficit * KV + ugw * ku);
+                qr = grad * ((ku * KV) * (deficit + ugw) / (deficit * KV + ugw * ku));
             }
         }
     }
@@ -689,46 +514,31 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     }
     if (i < nown) __builtin_nontemporal_store(is_lake ? 0. : CDIV_SY(q_infil - q_rech - Eu - Tu), atw(dy + nown, o8));
 
-#if SHUD_EDGE_PF == 2
-    // edge 0's neighbour gathers issued before the segment loop (in flight across it)
-    EdgeIn ein = load_edge<GH>(p, Y, mt.x >= 0 ? mt.x : i);
-#endif
     // ---- own river segments (fun_Seg_surface / fun_Seg_sub) and Qe2r (PassValue) ----
     const double dep = CLH(depression), rgh = CLH(rough);
     double qe2r_surf = 0., qe2r_sub = 0.;
-    if (nseg && !(SHUD_EABL & 1)) {
+    if (nseg) {
         const double isf_seg = rmax(0., usf - q_infil + q_exfil);
         for (int k = sfirst, k1 = k + nseg; k < k1; k++) {
-            // one 48-B element-sorted record per segment: its own fields plus its reach's statics
-            const uint32_t k16 = (uint32_t)k << 4;
-            [[maybe_unused]] const uint32_t k8 = (uint32_t)k << 3;
-#if SHUD_SEG_RREC
             // 20 B per segment streamed ({length, Cwr} + its reach); the reach's {depth, KsatH | BedThick, BC} is one
-            // 32-B record shared by the reach's ~5 segments (a gather beside the stage gather, mostly cache hits)
+            // 32-B record shared by the reach's ~5 segments (a gather beside the stage gather, mostly cache hits).
+            // (A 48-B segment record with the reach statics copied in, rounds 1-3: +153 MB of HBM per launch.)
+            const uint32_t k16 = (uint32_t)k << 4;
             const double2 lc = *at(p.sg_lc, k16);
             const int rr = *at(p.sg_r, (uint32_t)k << 2);
             const double2 dk = p.rrec[2 * (size_t)rr], rx = p.rrec[2 * (size_t)rr + 1];
-            const int2 rb = make_int2(rr, __builtin_bit_cast(int2, rx.y).x);
+            const int rbc = __builtin_bit_cast(int2, rx.y).x;
             const double bt = rx.x;
-#else
-            const double2 lc = *at(p.sg_lc, k16), dk = *at(p.sg_dk, k16);
-            const int2 rb = *at(p.sg_rb, k8);
-            const double bt = *at(p.sg_bt, k8);
-#endif
             // (the first segment's reach index + stage loaded at the top of the body instead, in flight across the
             // vertical physics: 88 VGPRs, 0.625 vs 0.623 ms — not kept, profiles/r03/ab_river2/)
-            double yr = GH ? Y.riv(rb.x) : *at(Y.y + 3 * (size_t)nown, (uint32_t)rb.x << 3);   // uriv_of, BC below
+            double yr = GH ? Y.riv(rr) : *at(Y.y + 3 * (size_t)nown, (uint32_t)rr << 3);   // uriv_of, BC below
             if (MODE == 1) yr = (yr >= 0.) ? yr : 0.;
-            if (rb.y > 0) yr = m.rybc[rb.y];
+            if (rbc > 0) yr = m.rybc[rbc];
             const double rdep = dk.x, L = lc.x;
             const double qs = weir_jtoi(zs, isf_seg, zs - rdep, yr, zs + 0.0, lc.y, L, dep);
-#if SHUD_RCP & 4
-            const double qg = r2e_gw<true>(yr, zs - rdep, ugw, zb, ekh, dk.y, L, bt, *at(p.sg_rbt, k8)) * fu_sub;
-#else
             const double qg = r2e_gw(yr, zs - rdep, ugw, zb, ekh, dk.y, L, bt) * fu_sub;
-#endif
-            if (p.seg_rpos) p.qseg2[p.seg_rpos[k]] = make_double2(qs, qg);
-            else *atw(p.qseg2, k16) = make_double2(qs, qg);                  // element-sorted (default)
+            if (WT) st_wt16(p.qseg2, k16, qs, qg);                       // element-sorted; river fold: write-through
+            else *atw(p.qseg2, k16) = make_double2(qs, qg);
             qe2r_surf += -qs;
             qe2r_sub += -qg;
         }
@@ -746,30 +556,11 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     double sumsurf = qe2r_surf, sumsub = qe2r_sub;     // QeleSurfTot = Qe2r + sum_j QeleSurf[j]
     bool nan_q = false;
     const double isf = usf < 0. ? 0. : usf;
-#if SHUD_AREA_EARLY
     const double area = ldnt(at(p.area, o8));          // in flight across the edge loop
-#endif
-    const int n_edges = (is_lake || (SHUD_EABL & 4)) ? 0 : 3;   // lake elements: fun_Ele_lakeHorizon, all zero
-#if SHUD_EDGE_PF == 1
-    // software-pipelined neighbour gathers: edge j+1's loads are issued at the top of edge j's iteration
-    EdgeIn ein;
-    if (n_edges) ein = load_edge<GH>(p, Y, mt.x >= 0 ? mt.x : i);
-#endif
+    const int n_edges = is_lake ? 0 : 3;               // lake elements: fun_Ele_lakeHorizon, all zero
 #pragma unroll 1
     for (int j = 0; j < n_edges; j++) {
         const int nb = j == 0 ? mt.x : j == 1 ? mt.y : mt.z;
-#if SHUD_EDGE_PF
-        const EdgeIn cur_e = ein;
-        if (j < 2) {
-            const int nb1 = j == 0 ? mt.y : mt.z;
-            ein = load_edge<GH>(p, Y, nb1 >= 0 ? nb1 : i);
-        }
-        const double2 g = ldnt2(at(p.ged + (size_t)j * NEl, o16));
-        const double2 nzz = cur_e.nzz;
-        const int ncf = cur_e.ncf;
-        const double nsf_raw = cur_e.nsf, ngw_raw = cur_e.ngw;
-        const int nc = nb >= 0 ? nb : i;
-#else
         const int nc = nb >= 0 ? nb : i;                  // boundary edge: harmless in-bounds loads
         // (edge 0's loads issued right after the own record instead — held through the vertical physics — took
         // the kernel to 96 VGPRs with spills and measured 0.707 vs 0.617 ms, profiles/r03/ab_prologue/)
@@ -779,25 +570,15 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
         const int ncf = *at((const int *)p.meta + 3, n16);
         const double nsf_raw = GH ? Y.sf(nc) : *at(Y.y, n8);
         const double ngw_raw = GH ? Y.gw(nc) : *at(Y.y + 2 * (size_t)nown, n8);
-#endif
         const double B = g.x, d2n = g.y;
-#if SHUD_RCP & 2
-        const double rd2n = ldnt(at(p.r_d2n + (size_t)j * NEl, o8));
-#define D2N_DIV(a) CDIV_(a, d2n, rd2n)
-#else
-#define D2N_DIV(a) SDIV(a, d2n)
-#endif
+        const Recip R2 = recip_nr(d2n);                   // both Dist2Nabor divisions of the edge share 1/d2n
         double qsf = 0., qsb = 0.;
         const int cn = cf_class(ncf);
 #define CN(f) (LCT ? lct[cn * CF_LDS_STRIDE + CfPos<CF_##f>::v] : p.ctab[cn * CF_STRIDE + CfPos<CF_##f>::v])
         double hvn[4] = {0., 0., 0., 0.};                 // HYB: the neighbour's streamed fields (if it reads any)
-        if (HYB == 1 && !(SHUD_HYBABL & 1) && p.hnb) hvn[0] = p.hv[nc];
-        else if (HYB == 2 && !(SHUD_HYBABL & 1) && p.hnb) hload(p, nc, hvn);
-#if SHUD_HYBSEL
-#define CNH(f) ((HYB && !(SHUD_HYBABL & 1)) ? hpick(hvn, p.hslot1[CF_##f], CN(f)) : CN(f))
-#else
-#define CNH(f) ((HYB && !(SHUD_HYBABL & 1) && p.hslot1[CF_##f]) ? (HYB == 1 ? hvn[0] : hsel(hvn, p.hslot1[CF_##f])) : CN(f))
-#endif
+        if (HYB == 1 && p.hnb) hvn[0] = p.hv[nc];
+        else if (HYB == 2 && p.hnb) hload(p, nc, hvn);
+#define CNH(f) ((HYB && p.hslot1[CF_##f]) ? (HYB == 1 ? hvn[0] : hsel(hvn, p.hslot1[CF_##f])) : CN(f))
         if (LAKE && nb >= 0 && ncf < 0) {                 // bank edge: the neighbour is a lake element
             const int l = lk.lake_of[nb];
             const double zl = lk.bathy_y[lk.bathy_off[l]];               // lake[l].zmin = bathymetry.yi[0]
@@ -810,7 +591,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
             else if (dhg < 0. && yl <= 0.02) q = 0.;
             else {
                 const double ymg = (rmax(ugw, 0.) + rmax(yl, 0.)) * .5;
-                const double grad = D2N_DIV(dhg);
+                const double grad = div_nr(dhg, R2);
                 const double kmean = 0.5 * (ekh + CNH(KsatH));           // the lake element's u_effKH = KsatH
                 q = kmean * grad * ymg * B;
             }
@@ -826,7 +607,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
             double ym = ((isf + zs) > (nsf + zsn)) ? ((isf > dep) ? isf : 0.) : ((nsf > dep) ? nsf : 0.);
             ym = rmin(ym, K_MAXYSURF);
             if (ym > 0.) {
-                const double s = D2N_DIV(dh);
+                const double s = div_nr(dh, R2);
                 if (s > 0 && isf <= 0) qsf = 0.;
                 else if (s < 0 && nsf <= 0) qsf = 0.;
                 else qsf = manning(ym * B, 0.5 * (rgh + CNH(rough)), ym, s);  // avgRough, Element.cpp:253
@@ -838,11 +619,9 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
             if (dhg > 0. && ugw <= 0.02) q = 0.;
             else if (dhg < 0. && ugn <= 0.02) q = 0.;
             else {
-                const double ekn = (SHUD_EABL & 2) ? CNH(KsatH)
-                                                   : eff_kh(ugn, zsn - zbn, CNH(macD), CNH(macKsatH), CNH(vAreaF),
-                                                            CNH(KsatH));
+                const double ekn = eff_kh(ugn, zsn - zbn, CNH(macD), CNH(macKsatH), CNH(vAreaF), CNH(KsatH));
                 const double ymg = (rmax(ugw, 0.) + rmax(ugn, 0.)) * .5;
-                const double grad = D2N_DIV(dhg);
+                const double grad = div_nr(dhg, R2);
                 const double kmean = 0.5 * (ekh + ekn);
                 q = kmean * grad * ymg * B;
             }
@@ -864,7 +643,6 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
         }
 #undef CN
 #undef CNH
-#undef D2N_DIV
         if (MODE == 0) nan_q |= nan_or_inf(qsf) || nan_or_inf(qsb);
         sumsurf += qsf;
         sumsub += qsb;
@@ -875,29 +653,20 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     if (MODE == 0) REPORT(nan_q, 0x01u, 0, false);         // CheckNANij, MD_f.cpp:73-74
 
     // ---- f_applyDY element part (MD_f.cpp:88-150 / MD_f_omp.cpp:26-46) ----
-#if !SHUD_AREA_EARLY
-    const double area = ldnt(at(p.area, o8));
-#endif
-#if SHUD_RCP & 1
-    const double rarea = ldnt(at(p.r_area, o8));
-#define AREA_DIV(a) CDIV_(a, area, rarea)
-#else
-#define AREA_DIV(a) SDIV(a, area)
-#endif
     double dsf, dgw;
+    const Recip RA = recip_nr(area);                          // the area divisions share 1/area
     if (LSP) {
         const double es = lsp[0], eg = lsp[kEleBS], tg = lsp[2 * kEleBS], dsh = lsp[3 * kEleBS], dgh = lsp[4 * kEleBS];
-        dsf = dsh - AREA_DIV(sumsurf) - es;
-        dgw = dgh - AREA_DIV(sumsub) - eg - tg;
+        dsf = dsh - div_nr(sumsurf, RA) - es;
+        dgw = dgh - div_nr(sumsub, RA) - eg - tg;
     } else {
-        dsf = dsf_head - AREA_DIV(sumsurf) - Es;
-        dgw = dgw_head - AREA_DIV(sumsub) - Eg - Tg;
+        dsf = dsf_head - div_nr(sumsurf, RA) - Es;
+        dgw = dgw_head - div_nr(sumsub, RA) - Eg - Tg;
     }
     const int cf_t = LSP ? lspi[0] : cf;                      // (LSP: the cf word back from LDS)
     const int ibc_t = LSP ? cf_ibc(cf_t) : ibc, iss_t = LSP ? cf_iss(cf_t) : iss;
     if (ibc_t > 0) dgw = 0;
-    else if (ibc_t < 0) dgw += AREA_DIV(m.eqbc[-ibc_t]);
-#undef AREA_DIV
+    else if (ibc_t < 0) dgw += div_nr(m.eqbc[-ibc_t], RA);
     if (iss_t == 1) dsf += zero_over(area);                   // QSS is never assigned: 0.0 / area
     else if (iss_t == 2) dgw += zero_over(area);
     dgw = CDIV_SY(dgw);
@@ -962,7 +731,7 @@ __device__ __forceinline__ double riv_down_outlet(const RivP &q, double uq, cons
 // HALO (the folded partition launch): a wave with a lane whose reach or downstream is a ghost takes the halo
 // wait (poll + agent acquire, which invalidates the CU's L1) before its stage loads; the others — nearly all —
 // read only owned stages and skip it.  r < 0: an idle lane (still reaches the wave-wide ballot).
-template <int MODE, bool HALO>
+template <int MODE, bool HALO, bool WT>
 __device__ __forceinline__ void qd_pre(const DevMesh &m, const DevPacked &p, const YView &Y, int r, int n_int,
                                        const HaloWait *hw) {
     const int rr = r < 0 ? 0 : r;
@@ -979,14 +748,12 @@ __device__ __forceinline__ void qd_pre(const DevMesh &m, const DevPacked &p, con
     const double2 bd = p.rv[4 * (size_t)d + 1], dd = p.rv[4 * (size_t)d + 3];
     double ydg;
     const double ud = riv_stage_p<MODE>(m, Y, d, rv_ib(dd.y).y, &ydg);
-    p.qdown[r] = riv_down_p(q, ur, g, ud, dd.x, bd.y);
+    const double qd = riv_down_p(q, ur, g, ud, dd.x, bd.y);
+    if (WT) __hip_atomic_store((unsigned long long *)p.qdown + r, __builtin_bit_cast(unsigned long long, qd),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // write-through (sc1): river fold
+    else p.qdown[r] = qd;
 }
 
-// ABL (timing-only ablation builds, -DSHUD_RIV_ABL=k; results are wrong when != 0): bit 0 skips the upstream
-// reaches, bit 1 the segment gathers, bit 2 the downstream reach
-#ifndef SHUD_RIV_ABL
-#define SHUD_RIV_ABL 0
-#endif
 // dword-aligned 16-B / 8-B loads of index words (gfx950 global loads need only 4-B alignment for dwordx4)
 struct __attribute__((packed, aligned(4))) Int4u { int x, y, z, w; };
 struct __attribute__((packed, aligned(4))) Int2u { int x, y; };
@@ -997,13 +764,9 @@ struct __attribute__((packed, aligned(4))) Int2u { int x, y; };
 // together from the offset in that word (no up_off load, no index load per upstream reach); a segment batch's
 // flux positions as 16-B (+ 8-B) loads instead of one 4-B load each; SB segments per batch, chosen by the host
 // from the reaches' segment counts (choose_riv_sb, shud_rhs.cpp).  0.0709 -> 0.0605 ms at syn-10M, same bits.
-template <int MODE, bool DIAG, int SB, bool QD, int ABL = 0>
-__global__ void __launch_bounds__(256)
-shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, DevDiag dg, int per8) {
-    // XCD-chunked workgroup order: a reach's up/downstream records sit a few blocks away in index space,
-    // so they are L2 hits on the same XCD instead of fabric round trips (speed only)
-    const int r = tile_of(per8) * 256 + (int)threadIdx.x;
-    if (r >= Y.n_own_riv) return;
+template <int MODE, bool DIAG, int SB, bool QD>
+__device__ __forceinline__ void riv_body(const DevMesh &m, const DevPacked &p, const YView &Y, double *__restrict__ dy,
+                                         const DevDiag &dg, int r) {
     const RivP q = riv_load(p, r);
     const int4 ru = p.rv_u[r];                  // {first segment, #segments | code << 16, w2, w3}
     const int seg0 = ru.x, nseg = ru.y & 0xffff, upc = ru.y >> 16;
@@ -1011,8 +774,7 @@ shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     const double ur = riv_stage_p<MODE>(m, Y, r, q.bc, &yg);
     const RivGeom g = riv_geom_p(q, yg);
     double qdown = 0.;
-    if (ABL & 4) {
-    } else if (QD) {
+    if (QD) {
         qdown = p.qdown[r];                                     // this eval's pre-pass (qd_pre), same operands
     } else {
         const int d = q.down >= 0 ? q.down : r;                 // clamped: unconditional loads
@@ -1033,8 +795,7 @@ shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
         return -riv_down_p(qu, uu, riv_geom_p(qu, yu), ur, q.depth, q.slope);
     };
     double qup = 0.;
-    if (ABL & 1) {
-    } else if (upc < 3) {                                       // 0..2 upstream reaches in w2, w3
+    if (upc < 3) {                                       // 0..2 upstream reaches in w2, w3
         if (upc > 0) qup += up_term(ru.z);
         if (upc > 1) qup += up_term(ru.w);
     } else {                                                    // more: up_idx[w2 .. w2 + w3), 8 indices at a time
@@ -1052,14 +813,6 @@ shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     // the positions (16-B loads; rseg_pos is padded by 8 words), then all gathers, are in flight together;
     // positions past the reach's last segment are replaced by its first (the same line); the adds stay in order
     double qsurf = 0., qsub = 0.;
-    if (ABL & 2) {
-    } else if (p.seg_rpos) {                            // reach-sorted fluxes: this reach's segments are contiguous
-        for (int k = seg0, k1 = seg0 + nseg; k < k1; k++) {
-            const double2 q2 = p.qseg2[k];
-            qsurf += q2.x;
-            qsub += q2.y;
-        }
-    } else
     for (int k0 = seg0, k1 = seg0 + nseg; k0 < k1; k0 += SB) {
         int raw[SB], ps[SB];
 #pragma unroll
@@ -1093,20 +846,122 @@ shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     dy[3 * Y.n_own + r] = dv;
     if (DIAG) { dg.qriv_down[r] = qdown; dg.qriv_up[r] = qup; dg.qriv_surf[r] = qsurf; dg.qriv_sub[r] = qsub; }
 }
+template <int MODE, bool DIAG, int SB, bool QD>
+__global__ void __launch_bounds__(256)
+shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, DevDiag dg, int per8) {
+    // XCD-chunked workgroup order: a reach's up/downstream records sit a few blocks away in index space,
+    // so they are L2 hits on the same XCD instead of fabric round trips (speed only)
+    const int r = tile_of(per8) * 256 + (int)threadIdx.x;
+    if (r >= Y.n_own_riv) return;
+    riv_body<MODE, DIAG, SB, QD>(m, p, Y, dy, dg, r);
+}
+
+// ===================================================================================
+// River fold: elements, QrivDown pre-pass and reaches in ONE launch (unpartitioned, lake-free, LDS class table).
+// Blocks [0, nb_e + nb_q) are the element tiles and the QrivDown blocks of the single launch; the reach tiles follow in
+// blocks nb_e + nb_q .. (DevPacked::rf_tile: in the order their inputs come due), so a reach tile whose elements are
+// done runs in the slots the element launch's tail leaves idle instead of after it (the river kernel was 7 % of every
+// RHS, latency-bound on dependent gathers).  Hand-off (MI355X guide Guideline 16 R1): every element tile and QrivDown
+// block stores its qseg2 / qdown results write-through (sc1), drains them (vmcnt(0) in every wave), meets a workgroup
+// barrier, and one lane stores the eval's epoch into its flag (agent scope); a reach tile's wave 0 polls the flags of
+// the element tiles owning every 128-B qseg2 line it reads and of the QrivDown blocks of its own and upstream reaches
+// (DevPacked::rf_dep, host-computed), then ONE agent acquire, a workgroup barrier, plain loads.  Reach tiles sit after
+// every element and QrivDown block, so once dispatched, all they wait for is resident or done; the poll is bounded all
+// the same (wall clock, then the fatal SHUD_EF_HALO_WAIT).  Same arithmetic as the two launches: bit-identical.
+// ===================================================================================
+#ifndef SHUD_RF_DIAG
+#define SHUD_RF_DIAG 0      // TEMP timing-only: 1 no poll, 2 no publish + no poll, 4 plain stores
+#endif
+__device__ __forceinline__ void rf_publish(unsigned *flag, unsigned epoch) {
+    if (SHUD_RF_DIAG & 2) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // every wave: its write-through stores are out
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// each wave drains its own stores and counts itself in an LDS word; the wave that completes the count publishes (MI355X
+// guide Valid forms, Producer: "each wave adds to a counter in LDS after its wait and the wave whose add is last
+// signals") — no workgroup barrier at the end, so early waves leave as soon as their own stores are out
+__device__ __forceinline__ void rf_publish_lds(unsigned *flag, unsigned epoch, unsigned *cnt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned old = 0;
+    if (__lane_id() == 0) old = atomicAdd(cnt, 1u);
+    old = __shfl(old, 0);
+    if (old == (kEleBS / 64) - 1 && __lane_id() == 0)
+        __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <int MODE>
+__device__ __forceinline__ void rf_reach_tile(const DevMesh &m, const DevPacked &p, const YView &Y, double *__restrict__ dy,
+                                              const DevDiag &dg, int tile, int nb_e, unsigned epoch,
+                                              unsigned long long timeout) {
+    if (!(SHUD_RF_DIAG & 3) && threadIdx.x < 64) {            // wave 0 polls every flag this tile's inputs carry
+        const int4 d = p.rf_dep[tile];
+        const int ne = d.y - d.x + 1, n = ne + (d.w - d.z + 1);
+        const int lane = (int)threadIdx.x;
+        const unsigned long long t0 = wall_clock64();
+        bool late = false;
+        for (;;) {
+            bool ok = true;
+            for (int k = lane; k < n; k += 64) {
+                const int f = k < ne ? d.x + k : nb_e + d.z + (k - ne);
+                ok &= __hip_atomic_load(p.rf_flag + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+            }
+            if (__builtin_amdgcn_ballot_w64(!ok) == 0ull) break;
+            if (wall_clock64() - t0 > timeout) { late = true; break; }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        report_w(m.err, late, 0x80u, 7, tile * 256);           // SHUD_EF_HALO_WAIT (a timed-out wait)
+    }
+    __syncthreads();
+    const int r = tile * 256 + (int)threadIdx.x;
+    if (r < Y.n_own_riv) riv_body<MODE, false, 6, true>(m, p, Y, dy, dg, r);
+}
+template <int MODE, bool OPEN, bool FU1, int LSPK>
+__global__ void __launch_bounds__(kEleBS, kEleWaves)
+shud_rhs_kernel_packed_rf(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int n_compute, int cur, DevDiag dg,
+                          int per8, int nb_e, int nb_q, int q0, unsigned epoch, unsigned long long timeout) {
+    extern __shared__ double lct[];
+    const int b = (int)blockIdx.x;
+    if (b >= nb_e + nb_q) {
+        rf_reach_tile<MODE>(m, p, Y, dy, dg, p.rf_tile[b - nb_e - nb_q], nb_e, epoch, timeout);
+        return;
+    }
+    int eb = b;
+    const int qb = qd_split(b, nb_q, q0, &eb);
+    if (qb >= 0) {
+        const int r = qb * kEleBS + (int)threadIdx.x;
+        if (r < p.nqd) qd_pre<MODE, false, !(SHUD_RF_DIAG & 4)>(m, p, Y, r, 0, nullptr);
+        rf_publish(p.rf_flag + nb_e + qb, epoch);
+        return;
+    }
+    const int t = tile_of(per8, eb);
+    const int i = t * kEleBS + (int)threadIdx.x;
+    const bool act = i < n_compute;
+    const DevLake lk{};
+    double tv[kTabBatch];
+    tab_issue<kEleBS>(p, tv);
+    OwnRec own;
+    if (act) own = load_own<FU1, false>(p, Y, i, cur);
+    tab_store<kEleBS>(p, tv, lct);
+    unsigned *cnt = (unsigned *)(lct + p.ntab + (LSPK ? kLspN * kEleBS + kEleBS / 2 : 0));   // after the tables / slots
+    if ((SHUD_RF_DIAG & 8) && threadIdx.x == 0) *cnt = 0u;
+    if (p.rf_dbg_ticks && t == p.rf_dbg_tile && threadIdx.x == 0) {   // test hook: a late element tile
+        const unsigned long long t0 = wall_clock64();
+        while (wall_clock64() - t0 < p.rf_dbg_ticks) __builtin_amdgcn_s_sleep(8);
+    }
+    __syncthreads();
+    if (act) ele_body<MODE, OPEN, false, FU1, true, false, false, 0, LSPK, !(SHUD_RF_DIAG & 4)>(m, p, Y, dy, i, cur, dg, lk,
+                                                                                              lct, own);
+    if (SHUD_RF_DIAG & 8) rf_publish_lds(p.rf_flag + t, epoch, cnt);
+    else rf_publish(p.rf_flag + t, epoch);
+}
 
 template <int SB, bool QD>
 static void launch_riv_sb(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int mode, bool diag,
                           const DevDiag &dg, hipStream_t s) {
     const dim3 grid(((Y.n_own_riv + 255) / 256 + 7) / 8 * 8), blk(256);
     const int per8 = (int)grid.x / 8;
-#if SHUD_RIV_ABL
-    // timing-only ablation build (tools/riv_abl.sh: -DSHUD_RIV_ABL=k); never part of the production library
-    if (mode == 0 && !diag) {
-        hipLaunchKernelGGL((shud_riv_kernel_packed<0, false, SB, QD, SHUD_RIV_ABL>), grid, blk, 0, s, m, p, Y, dy, dg,
-                           per8);
-        return;
-    }
-#endif
     if (mode == 0) {
         if (diag) hipLaunchKernelGGL((shud_riv_kernel_packed<0, true, SB, QD>), grid, blk, 0, s, m, p, Y, dy, dg, per8);
         else hipLaunchKernelGGL((shud_riv_kernel_packed<0, false, SB, QD>), grid, blk, 0, s, m, p, Y, dy, dg, per8);
@@ -1258,37 +1113,21 @@ static size_t lds_bytes(const DevPacked &p, bool lct, bool lspk) {
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB = 0, int LSPK = 0>
 static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1, int cur,
                      const DevDiag &dg, const DevLake &lk, hipStream_t s, int nq = 0) {
-    int nb = (i1 - i0 + kEleBS * kTiles - 1) / (kEleBS * kTiles);
+    int nb = (i1 - i0 + kEleBS - 1) / kEleBS;
     nb = (nb + 7) / 8 * 8;                  // block_id<1> deals blocks to XCDs in contiguous chunks
     const int nbq = nq > 0 ? ((nq + kEleBS - 1) / kEleBS + 7) / 8 * 8 : 0;
     const int q0 = qd_start(nb, p.qd_pm);
     const size_t lds = lds_bytes(p, LCT, LSPK != 0);
-    if constexpr (SHUD_PERSIST != 0) {
-        auto *fn = shud_ele_kernel_persist<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH, HYB>;
-        static int slots = 0;                   // resident workgroups per XCD (per instantiation)
-        if (!slots) {
-            int dev = 0, ncu = 0, per_cu = 0;
-            (void)hipGetDevice(&dev);
-            (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)fn, kEleBS, lds);
-            slots = std::max(1, ncu * std::max(per_cu, 1) / 8);
-        }
-        const int g = 8 * std::min(slots, nb / 8);
-        const int nqt = nq > 0 ? (nq + kEleBS - 1) / kEleBS : 0;
-        const PersistArgs pa{m, p, Y, dy, dg, lk, i0, i1, cur, nb / 8, nqt};
-        hipLaunchKernelGGL(fn, dim3(g), dim3(kEleBS), lds, s, pa);
-        return;
-    }
     hipLaunchKernelGGL((shud_ele_kernel_packed<MODE, OPEN, DIAG, FU1, LCT, LAKE, GH, HYB, LSPK>), dim3(nb + nbq), dim3(kEleBS),
                        lds, s,
                        m, p, Y, dy, i0, i1, cur, dg, lk, nb / 8, nbq, q0);
 }
 
-// the plain LDS-table instantiation, with the DY-tail values parked in LDS when 7 workgroups still fit (SHUD_LSPILL)
+// the plain LDS-table instantiation, with the DY-tail values parked in LDS when 7 workgroups still fit (LSP)
 template <int MO, bool OP, bool DI, bool FU, bool GH>
 static void launch_plain(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1, int cur,
                          const DevDiag &dg, const DevLake &lk, hipStream_t s, int nq) {
-    if constexpr (!DI && SHUD_LSPILL != 0) {
+    if constexpr (!DI) {
         if (lds_bytes(p, true, true) <= kLspLdsMax) {
             launch_p<MO, OP, DI, FU, true, false, GH, 0, 1>(m, p, Y, dy, i0, i1, cur, dg, lk, s, nq);
             return;
@@ -1351,11 +1190,11 @@ bool launch_element_kernel_packed_fold(const DevMesh &m, const DevPacked &p, con
     // QrivDown blocks among the interior tiles (they wait for the halo like the boundary ones: it has normally
     // arrived long before), pm of the interior blocks before them
     const int q0 = qd_start(nb_int, p.qd_pm_fold);
-    // the DY-tail LDS slots as in the single launch (SHUD_LSPILL), while 7 workgroups still fit
-    const bool lsp = SHUD_LSPILL != 0 && lds_bytes(p, true, true) <= kLspLdsMax;
+    // the DY-tail LDS slots as in the single launch (LSP), while 7 workgroups still fit
+    const bool lsp = lds_bytes(p, true, true) <= kLspLdsMax;
     const size_t lds = lds_bytes(p, true, lsp);
 #define LF(MO, OP, FU) do {                                                                                        \
-        if (lsp) hipLaunchKernelGGL((shud_ele_kernel_packed_fold<MO, OP, FU, SHUD_LSPILL ? 1 : 0>),                \
+        if (lsp) hipLaunchKernelGGL((shud_ele_kernel_packed_fold<MO, OP, FU, 1>),                \
                                     dim3(nb_int + nb_b + nbq), dim3(256), lds, s, m, p, Y, dy, n_int, n_all, cur, dg, \
                                     nb_int / 8, nb_int, hw, nbq, q0);                                              \
         else hipLaunchKernelGGL((shud_ele_kernel_packed_fold<MO, OP, FU>), dim3(nb_int + nb_b + nbq), dim3(256),    \
@@ -1381,6 +1220,33 @@ void launch_copy_f64(double *dst, const double *src, size_t n, hipStream_t s) {
     if (!n) return;
     const size_t nb = std::min<size_t>((n + 255) / 256, 4096);
     hipLaunchKernelGGL(shud_copy_f64_kernel, dim3((unsigned)nb), dim3(256), 0, s, dst, src, n);
+}
+
+bool launch_rhs_packed_rf(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int n, int cur, int mode,
+                          bool open, bool fu_unit, const DevDiag &dg, unsigned epoch, unsigned long long timeout,
+                          hipStream_t s) {
+    if (n <= 0 || p.rf_ntile <= 0 || !p.rf_flag || !p.qdown || p.nqd <= 0 || p.ncls > LDS_CLS_MAX || p.nh ||
+        Y.gele || Y.griv)
+        return false;
+    const EleGrid g = ele_grid(n, p.nqd, p.rf_qd_pm);
+    const bool lsp = lds_bytes(p, true, true) + 16 <= kLspLdsMax;
+    const size_t lds = lds_bytes(p, true, lsp) + 16;                 // + the workgroup's publish counter
+    const dim3 grid(g.nb_e + g.nb_q + p.rf_ntile), blk(kEleBS);
+#define RF(MO, OP, FU) do {                                                                                      \
+        if (lsp) hipLaunchKernelGGL((shud_rhs_kernel_packed_rf<MO, OP, FU, 1>), grid, blk, lds, s, m, p, Y, dy, n,  \
+                                    cur, dg, g.per8(), g.nb_e, g.nb_q, g.q0, epoch, timeout);                    \
+        else hipLaunchKernelGGL((shud_rhs_kernel_packed_rf<MO, OP, FU, 0>), grid, blk, lds, s, m, p, Y, dy, n, cur, \
+                                dg, g.per8(), g.nb_e, g.nb_q, g.q0, epoch, timeout);                             \
+    } while (0)
+    if (mode == 0) {
+        if (open) { if (fu_unit) RF(0, true, true); else RF(0, true, false); }
+        else { if (fu_unit) RF(0, false, true); else RF(0, false, false); }
+    } else {
+        if (open) { if (fu_unit) RF(1, true, true); else RF(1, true, false); }
+        else { if (fu_unit) RF(1, false, true); else RF(1, false, false); }
+    }
+#undef RF
+    return true;
 }
 
 void launch_pack_step_kernel(const DevMesh &m, const DevPacked &p, int n, int cur, unsigned what, hipStream_t s) {

@@ -52,12 +52,16 @@ struct shud_rhs {
     bool have_diag = false;
     int cur = 0, cur_e = 0;
     long long ncalls = 0;
-    int variant = 0;                     // element-kernel build variant (SHUD_RHS_ELE_VARIANT, A/B only)
     bool packed = false;                 // class-table / 16-byte-record layout in use (DevPacked)
     DevPacked dp{};
     int n_classes = 0;
     bool fu_unit[2] = {true, true};      // fu_Surf / fu_Sub are all 1.0 (cryosphere off): not read
     bool qd_now = false;                 // this eval's element launch wrote DevPacked::qdown (river kernel reads it)
+    // river fold (build_river_fold): the eval's flag value (never 0), the reach tiles' poll bound, whether the last
+    // ordinary eval took the folded launch (its element-kernel time then includes the reaches)
+    unsigned rf_epoch = 0;
+    unsigned long long rf_timeout = 0;
+    bool rf_now = false;
 
     // host-pointer eval staging
     double *d_y = nullptr, *d_ydot = nullptr, *d_scratch_dy = nullptr;
@@ -67,7 +71,6 @@ struct shud_rhs {
     int last_cur = 0, last_cur_e = 0;
 
     std::vector<int> seg_perm;           // element-sorted position -> reference segment index
-    std::vector<int> rseg_perm;          // reach-sorted position -> reference segment index (SEG_ORDER=reach)
     int max_col[4] = {0, 0, 0, 0};       // highest BC column referenced: eyBC, eqBC, ryBC, rqBC
     double *d_tab[4] = {nullptr, nullptr, nullptr, nullptr};
     int tab_len[4] = {0, 0, 0, 0};

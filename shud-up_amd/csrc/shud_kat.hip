@@ -3,6 +3,9 @@
 // tuples, ids and argument order as oracle_kat() (oracle/shud_oracle.c).  tests/test_kat.py compares.
 #include <hip/hip_runtime.h>
 #include <vector>
+// the fast sqrt / shared-reciprocal division paths of shud_physics.h, whatever the kernels' build defaults
+#define SHUD_SQRT_NR 1
+#define SHUD_DIV_NR 1
 #include "shud_physics.h"
 
 using namespace shud;
@@ -40,13 +43,12 @@ __global__ void kat_kernel(int fn, int k, const double *__restrict__ in, int n, 
     out[t] = r;
 }
 
-// pow_pos / pow_tab (shud_physics.h, shud_powtab.h) next to OCML's full pow on the same (x, y) pairs: which = 0 pow,
-// 1 pow_pos, 2 pow_tab
+// pow_tab (shud_powtab.h) next to OCML's full pow on the same (x, y) pairs: which = 0 pow, 2 pow_tab
 __global__ void kat_pow_kernel(int which, const double *__restrict__ xy, int n, double *__restrict__ out) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
     const double x = xy[2 * t], y = xy[2 * t + 1];
-    out[t] = which == 2 ? shud_pow_tab(x, y) : which ? pow_pos(x, y) : pow(x, y);
+    out[t] = which == 2 ? shud_pow_tab(x, y) : pow(x, y);
 }
 extern "C" int shud_kat_pow(int which, const double *h_xy, int n, double *h_out) {
     if (n <= 0) return -1;
@@ -154,6 +156,40 @@ extern "C" void shud_kat_ode_free(void *user) {
     (void)hipStreamSynchronize(u->s);
     (void)hipStreamDestroy(u->s);
     delete u;
+}
+
+// sqrt_nr / div_nr (shud_physics.h) next to the device's own sqrt and IEEE division on the same operands: which = 0
+// sqrt_nr(a), 1 sqrt(a), 2 div_nr(a, recip_nr(b)), 3 a / b, 4 cbrt_glibc(a)
+__global__ void kat_fast_kernel(int which, const double *__restrict__ a, const double *__restrict__ b, int n,
+                                double *__restrict__ out) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    double r;
+    switch (which) {
+        case 0: r = sqrt_nr(a[t]); break;
+        case 1: r = sqrt(a[t]); break;
+        case 2: r = div_nr(a[t], recip_nr(b[t])); break;
+        case 4: r = cbrt_glibc(a[t]); break;
+        default: r = a[t] / b[t]; break;
+    }
+    out[t] = r;
+}
+extern "C" int shud_kat_fast(int which, const double *h_a, const double *h_b, int n, double *h_out) {
+    if (n <= 0) return -1;
+    double *d = nullptr;
+    const size_t bytes = sizeof(double) * (size_t)n;
+    if (hipMalloc(&d, 3 * bytes) != hipSuccess) return -3;
+    int rc = 0;
+    if (hipMemcpy(d, h_a, bytes, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d + n, h_b, bytes, hipMemcpyHostToDevice) != hipSuccess)
+        rc = -3;
+    if (!rc) {
+        hipLaunchKernelGGL(kat_fast_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, which, d, d + n, n, d + 2 * (size_t)n);
+        if (hipGetLastError() != hipSuccess) rc = -3;
+    }
+    if (!rc && hipMemcpy(h_out, d + 2 * (size_t)n, bytes, hipMemcpyDeviceToHost) != hipSuccess) rc = -3;
+    (void)hipFree(d);
+    return rc;
 }
 
 // cdiv (shud_physics.h) on host-given (a, b) pairs with the host's correctly rounded rb = 1/b, as the handle

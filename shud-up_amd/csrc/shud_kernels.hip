@@ -13,7 +13,8 @@
 //                     its upstream reaches (the junction sum of PassValue MD_f.cpp:236-240 in ascending
 //                     reach order), segment sums in ascending segment order, river DY (MD_f.cpp:157-179).
 // Every reduction is evaluated in the reference's order, so results are deterministic and equal to
-// the serial reference up to libm (OCML vs glibc pow/cbrt/cos) rounding.
+// the serial reference up to libm (OCML vs glibc pow/cbrt/cos) rounding.  Same leaf functions as the packed kernel
+// (shud_physics.h: pow_tab for satKfun, OCML's cos on [0, pi] = cos_small), so both layouts give the same bits.
 // Compiled with -ffp-contract=off (the reference x86-64 -O3 build has no FMA).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -25,10 +26,10 @@ namespace shud {
 // ===================================================================================
 // element kernel
 // ===================================================================================
-template <int MODE, bool OPEN, bool DIAG, int VAR>
-__global__ void __launch_bounds__(256, LB<VAR>::w)
+template <int MODE, bool OPEN, bool DIAG>
+__global__ void __launch_bounds__(256)
 shud_ele_kernel(DevMesh m, YView Y, double *__restrict__ dy, int n_compute, int cur, int cur_e, DevDiag dg) {
-    const int i = block_id<VAR>() * blockDim.x + threadIdx.x;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_compute) return;
     const int NEl = m.num_ele;        // local element count (stride of per-edge arrays)
     const int nown = Y.n_own;
@@ -41,17 +42,17 @@ shud_ele_kernel(DevMesh m, YView Y, double *__restrict__ dy, int n_compute, int 
     if (MODE == 1) { usf = (usf >= 0.) ? usf : 0.; uus = (uus >= 0.) ? uus : 0.; }
     const double ugw = ugw_of<MODE>(m, Y, i, ibc);
 
-    const double aq = m.aq[i], infD = ld1<VAR>(&m.infD[i]), ThS = ld1<VAR>(&m.ThetaS[i]), ThR = ld1<VAR>(&m.ThetaR[i]);
-    const double infK = ld1<VAR>(&m.infKsatV[i]), hA = ld1<VAR>(&m.hAreaF[i]), macKV = ld1<VAR>(&m.macKsatV[i]);
-    const double fu_surf = ld1<VAR>(&m.fu_surf[i]), fu_sub = ld1<VAR>(&m.fu_sub[i]);
+    const double aq = m.aq[i], infD = m.infD[i], ThS = m.ThetaS[i], ThR = m.ThetaR[i];
+    const double infK = m.infKsatV[i], hA = m.hAreaF[i], macKV = m.macKsatV[i];
+    const double fu_surf = m.fu_surf[i], fu_sub = m.fu_sub[i];
 
     // ---- f_etFlux (MD_ET.cpp:343-404), serial semantics only ----
     double Es = 0., Eu = 0., Eg = 0., Tu = 0., Tg = 0., eic = 0., ibeta = 0.;
     if (MODE == 0) {
-        const double satn_prev = ld1<VAR>(&m.u_satn[cur][i]);
-        const double vf = ld1<VAR>(&m.VegFrac[i]), va = vf, vb = 1. - vf, pj = 1. - ld1<VAR>(&m.ImpAF[i]);
-        const double pet = ld1<VAR>(&m.pot_evap[i]), ptr = ld1<VAR>(&m.pot_tran[i]);
-        eic = ld1<VAR>(&m.e_ic[cur_e][i]);
+        const double satn_prev = m.u_satn[cur][i];
+        const double vf = m.VegFrac[i], va = vf, vb = 1. - vf, pj = 1. - m.ImpAF[i];
+        const double pet = m.pot_evap[i], ptr = m.pot_tran[i];
+        eic = m.e_ic[cur_e][i];
         {   // SoilMoistureStress is_sm_et.cpp:131-140
             double fc = ThS * K_FC_RATIO;
             double b = (satn_prev * (ThS - ThR) - ThR) / (fc - ThR);
@@ -63,13 +64,13 @@ shud_ele_kernel(DevMesh m, YView Y, double *__restrict__ dy, int n_compute, int 
             if (ugw > aq - infD) { Eg = rmin(rmax(0., ugw), pet - Es) * pj * vb; Eu = 0.; }
             else { Eg = 0.; Eu = rmin(rmax(0., uus), ibeta * (pet - Es)) * pj * vb; }
         }
-        if (ld1<VAR>(&m.lai[i]) > K_ZERO) {
+        if (m.lai[i] > K_ZERO) {
             if (eic >= ptr) { Tg = Tu = 0.; eic = ptr * pj * va; }
-            else if (ugw > aq - ld1<VAR>(&m.RzD[i])) { Tg = rmin(rmax(0., ugw), (ptr - eic)) * pj * va; Tu = 0.; }
+            else if (ugw > aq - m.RzD[i]) { Tg = rmin(rmax(0., ugw), (ptr - eic)) * pj * va; Tu = 0.; }
             else { Tg = 0.; Tu = rmin(rmax(0., uus), ibeta * (ptr - eic)) * pj * va; }
         } else { Tg = Tu = eic = 0.; }
         const double trans = Tg + Tu, evapo = Eu + Eg + Es, eta = eic + evapo + trans;
-        report_w(m.err, eta > ld1<VAR>(&m.etp[i]) * 2., 0x10u, 4, i, true);
+        report_w(m.err, eta > m.etp[i] * 2., 0x10u, 4, i, true);
         bool neg = false;
         neg |= (Es < 0.0 || isnan(Es) || isinf(Es) || fabs(Es - K_NA_VALUE) < K_ZERO);
         neg |= (Eu < 0.0 || isnan(Eu) || isinf(Eu) || fabs(Eu - K_NA_VALUE) < K_ZERO);
@@ -79,7 +80,7 @@ shud_ele_kernel(DevMesh m, YView Y, double *__restrict__ dy, int n_compute, int 
         report_w(m.err, neg, 0x04u, 2, i);
         report_w(m.err, !neg && (isnan(eta) || isinf(eta) || isnan(evapo) || isinf(evapo) || isnan(trans) || isinf(trans)),
                  0x08u, 3, i);
-        st1<VAR>(&m.e_ic[cur_e ^ 1][i], eic);
+        m.e_ic[cur_e ^ 1][i] = eic;
         if (DIAG) { dg.q_es[i] = Es; dg.q_eu[i] = Eu; dg.q_eg[i] = Eg; dg.q_tu[i] = Tu; dg.q_tg[i] = Tg;
                     dg.q_eta[i] = eta; dg.i_beta[i] = ibeta; }
     }
@@ -95,16 +96,23 @@ shud_ele_kernel(DevMesh m, YView Y, double *__restrict__ dy, int n_compute, int 
     if (satn > 0.99) { satn = 1.0; satkr = 1.0; theta = ThS; }
     else if (satn <= K_ZERO) { satn = 0.; satkr = 0.; theta = ThR; }
     else {   // satKfun Equations.cpp:136-141
-        const double n = ld1<VAR>(&m.Beta[i]);
-        const double tmp = -1. + pow(1. - pow(satn, n / (n - 1.)), (n - 1.) / n);
-        satkr = sqrt(satn) * tmp * tmp;
+        // Beta > 1 (every class the packed layout admits): the packed kernel's pow_tab, so both layouts give the same
+        // bits (shud_physics.h sat_kfun, tables from __constant__ memory); any other Beta: the full pow
+        const double n = m.Beta[i];
+        const double ex1 = n / (n - 1.), ex2 = (n - 1.) / n;
+        if (n > 1. && __builtin_isfinite(ex1) && __builtin_isfinite(ex2)) {
+            satkr = sat_kfun(satn, ex1, ex2);
+        } else {
+            const double tmp = -1. + pow(1. - pow(satn, ex1), ex2);
+            satkr = sqrt(satn) * tmp * tmp;
+        }
     }
-    st1<VAR>(&m.u_satn[cur ^ 1][i], satn);
+    m.u_satn[cur ^ 1][i] = satn;
 
     // ---- Flux_Infiltration (Element.cpp:271-303) ----
     double qi = 0., qex = 0.;
     {
-        const double av = usf + ld1<VAR>(&m.net_prep[i]);
+        const double av = usf + m.net_prep[i];
         if (ugw + uus > aq || deficit < uus) {
             qex = fabs(ugw + uus - aq) / aq * kmax;
         } else if (av > 0. && deficit > infD) {
@@ -120,7 +128,7 @@ shud_ele_kernel(DevMesh m, YView Y, double *__restrict__ dy, int n_compute, int 
     // ---- Flux_Recharge (Element.cpp:304-335) ----
     double qr = 0.;
     {
-        const double KV = ld1<VAR>(&m.KsatV[i]);
+        const double KV = m.KsatV[i];
         if (!(ugw > aq - infD && uus < deficit)) {
             double grad = 0.;
             if (theta > ThR && !(uus <= K_EPSILON)) {
@@ -136,7 +144,7 @@ shud_ele_kernel(DevMesh m, YView Y, double *__restrict__ dy, int n_compute, int 
     const double q_rech = qr * fu_sub;
 
     // ---- own river segments (fun_Seg_surface/fun_Seg_sub) and Qe2r (PassValue) ----
-    const double zs = m.z_surf[i], zb = m.z_bottom[i], dep = ld1<VAR>(&m.depression[i]);
+    const double zs = m.z_surf[i], zb = m.z_bottom[i], dep = m.depression[i];
     double qe2r_surf = 0., qe2r_sub = 0.;
     {
         const int k0 = m.seg_off[i], k1 = m.seg_off[i + 1];
@@ -168,8 +176,8 @@ shud_ele_kernel(DevMesh m, YView Y, double *__restrict__ dy, int n_compute, int 
     const double isf = usf < 0. ? 0. : usf;
 #pragma unroll
     for (int j = 0; j < 3; j++) {
-        const int nb = ld1<VAR>(&m.nabr[j * NEl + i]);
-        const double B = ld1<VAR>(&m.edge[j * NEl + i]);
+        const int nb = m.nabr[j * NEl + i];
+        const double B = m.edge[j * NEl + i];
         double qsf = 0., qsb = 0.;
         if (nb >= 0) {
             // surface (Manning)
@@ -177,7 +185,7 @@ shud_ele_kernel(DevMesh m, YView Y, double *__restrict__ dy, int n_compute, int 
             if (MODE == 1) nsf = (nsf >= 0.) ? nsf : 0.;
             nsf = nsf < 0. ? 0. : nsf;
             const double zsn = m.z_surf[nb];
-            const double d2n = ld1<VAR>(&m.dist2nabor[j * NEl + i]);
+            const double d2n = m.dist2nabor[j * NEl + i];
             const double dh = (isf + zs) - (nsf + zsn);
             double ym = ((isf + zs) > (nsf + zsn)) ? ((isf > dep) ? isf : 0.) : ((nsf > dep) ? nsf : 0.);
             ym = rmin(ym, K_MAXYSURF);
@@ -185,7 +193,7 @@ shud_ele_kernel(DevMesh m, YView Y, double *__restrict__ dy, int n_compute, int 
                 const double s = dh / d2n;
                 if (s > 0 && isf <= 0) qsf = 0.;
                 else if (s < 0 && nsf <= 0) qsf = 0.;
-                else qsf = manning(ym * B, ld1<VAR>(&m.avg_rough[j * NEl + i]), ym, s);
+                else qsf = manning(ym * B, m.avg_rough[j * NEl + i], ym, s);
             }
             // subsurface (Darcy); neighbour effKH recomputed from its own state (loop A value)
             const int fn = m.eflags[nb];
@@ -225,20 +233,20 @@ shud_ele_kernel(DevMesh m, YView Y, double *__restrict__ dy, int n_compute, int 
     if (MODE == 0) report_w(m.err, nan_q, 0x01u, 0, i);
 
     // ---- f_applyDY element part (MD_f.cpp:88-131 / MD_f_omp.cpp:26-46) ----
-    const double area = ld1<VAR>(&m.area[i]);
-    double dsf = ld1<VAR>(&m.net_prep[i]) - q_infil + q_exfil - sumsurf / area - Es;
+    const double area = m.area[i];
+    double dsf = m.net_prep[i] - q_infil + q_exfil - sumsurf / area - Es;
     double dus = q_infil - q_rech - Eu - Tu;
     double dgw = q_rech - q_exfil - sumsub / area - Eg - Tg;
     if (ibc > 0) dgw = 0;
     else if (ibc < 0) dgw += m.eqbc[-ibc] / area;
     if (iss == 1) dsf += 0.0 / area;          // QSS is never assigned (always 0)
     else if (iss == 2) dgw += 0.0 / area;
-    const double sy = ld1<VAR>(&m.Sy[i]);
+    const double sy = m.Sy[i];
     dus /= sy;
     dgw /= sy;
-    st1<VAR>(&dy[i], dsf);
-    st1<VAR>(&dy[nown + i], dus);
-    st1<VAR>(&dy[2 * nown + i], dgw);
+    dy[i] = dsf;
+    dy[nown + i] = dus;
+    dy[2 * nown + i] = dgw;
     if (DIAG) { dg.qele_surf_tot[i] = sumsurf; dg.qele_sub_tot[i] = sumsub; }
 }
 
@@ -351,14 +359,12 @@ shud_pack_kernel(const double *__restrict__ y, int n_own, int n_own_riv, const i
 }
 
 // ---- launchers ----
-template <int MODE, bool OPEN, bool DIAG, int VAR = 0>
+template <int MODE, bool OPEN, bool DIAG>
 static void launch_ele(const DevMesh &m, const YView &Y, double *dy, int n_compute, int cur, int cur_e,
                        const DevDiag &dg, hipStream_t s) {
     const int bs = 256;
     if (n_compute <= 0) return;
-    int nb = (n_compute + bs - 1) / bs;
-    if (VAR & 1) nb = (nb + 7) / 8 * 8;
-    hipLaunchKernelGGL((shud_ele_kernel<MODE, OPEN, DIAG, VAR>), dim3(nb), dim3(bs), 0, s,
+    hipLaunchKernelGGL((shud_ele_kernel<MODE, OPEN, DIAG>), dim3((n_compute + bs - 1) / bs), dim3(bs), 0, s,
                        m, Y, dy, n_compute, cur, cur_e, dg);
 }
 template <int MODE, bool DIAG>
@@ -370,15 +376,7 @@ static void launch_riv(const DevMesh &m, const YView &Y, double *dy, const DevDi
 }
 
 void launch_element_kernel(const DevMesh &m, const YView &Y, double *dy, int n_compute, int cur, int cur_e,
-                           int mode, bool open, bool diag, const DevDiag &dg, hipStream_t s, int variant) {
-    if (mode == 0 && !open && !diag && variant) {   // A/B variants of the production configuration
-        switch (variant) {
-#define V(k) case k: launch_ele<0, false, false, k>(m, Y, dy, n_compute, cur, cur_e, dg, s); return;
-            V(1) V(2) V(3) V(4) V(5) V(7) V(8) V(9) V(11)
-#undef V
-            default: break;
-        }
-    }
+                           int mode, bool open, bool diag, const DevDiag &dg, hipStream_t s) {
 #define L(MO, OP, DI) launch_ele<MO, OP, DI>(m, Y, dy, n_compute, cur, cur_e, dg, s)
     if (mode == 0) {
         if (open) { if (diag) L(0, true, true); else L(0, true, false); }

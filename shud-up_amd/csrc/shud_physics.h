@@ -7,53 +7,18 @@
 #include "shud_dev.h"
 #include "shud_powtab.h"
 
-// SHUD_ABL (timing-only ablation builds, never shipped): bit 0 pow, 1 cos, 2 cbrt, 3 division, 4 sqrt are
-// replaced by a single cheap op so their share of the element kernel's time can be measured.
-#ifndef SHUD_ABL
-#define SHUD_ABL 0
-#endif
-#if SHUD_ABL & 1
-#define SPOW(a, b) ((a) * (b))
-#else
-#define SPOW(a, b) pow(a, b)
-#endif
-#if SHUD_ABL & 2
-#define SCOS(a) (a)
-#else
-#define SCOS(a) cos(a)
-#endif
-#if SHUD_ABL & 4
-#define SCBRT(a) (a)
-#else
-#define SCBRT(a) cbrt(a)
-#endif
-#if SHUD_ABL & 8
-#define SDIV(a, b) ((a) * (b))
-#else
-#define SDIV(a, b) ((a) / (b))
-#endif
-#if SHUD_ABL & 16
-#define SSQRT(a) (a)
-#else
-#define SSQRT(a) sqrt(a)
-#endif
-
 namespace shud {
 
-// a / b for a class-constant divisor b with its host-computed, correctly rounded reciprocal rb (SHUD_CDIV=1):
+// a / b for a class-constant divisor b with its host-computed, correctly rounded reciprocal rb:
 // q0 = a*rb is within 1 ulp of a/b, the residual a - q0*b is exact in one fma, and one fma correction then
 // rounds to nearest exactly like IEEE division (Markstein's theorem; round-to-nearest, no under/overflow).
 // Exact, zero, infinite and NaN residuals keep q0 (signed zeros and infinities as a/b gives them).
-// SHUD_CDIV=0 uses the plain division (A/B: identical results, CDIV=1 measured 1 % faster on syn-10M).
 // Range: the handle admits a divisor only when it is 0, +-inf, NaN or 2^-20 <= |b| <= 2^20 (kCdivBmin/Bmax,
 // checked at create); then for 2^-948 <= |a| <= 2^1000 neither q0 nor the residual leaves the normal range and
 // the theorem holds.  Outside that numerator range (tiny non-zero or huge a: subnormal quotients, overflow of
 // a*rb) the exec-masked cold path takes the IEEE division itself, so cdiv(a, b, RN(1/b)) == a / b for every a
 // (tests/test_kat.py::test_cdiv_bit_identical on subnormal, near-overflow, signed-zero and special operands).
 // Zero, infinite and NaN numerators and 0/inf/NaN divisors stay on the fast path: q0 is then already a / b.
-#ifndef SHUD_CDIV
-#define SHUD_CDIV 1
-#endif
 __device__ __forceinline__ double cdiv(double a, double b, double rb) {
     const double q0 = a * rb;
     const double e = __builtin_fma(-q0, b, a);
@@ -63,11 +28,74 @@ __device__ __forceinline__ double cdiv(double a, double b, double rb) {
     if (__builtin_expect((aa < 0x1p-948 && a != 0.) || aa > 0x1p1000, 0)) q = a / b;
     return q;
 }
-#if SHUD_CDIV && !(SHUD_ABL & 8)
-#define CDIV_(a, b, rb) cdiv(a, b, rb)
-#else
-#define CDIV_(a, b, rb) SDIV(a, b)
+
+// ---- the compiler's correctly rounded f64 sqrt and division, without their range repairs on the common range ----
+// sqrt: LLVM's gfx9 lowering is y = rsq(x'), g = x' y, h = y / 2, two Newton-Raphson steps on (g, h), where x' = x or,
+// for x < 2^-767, x 2^256 (result scaled back by 2^-128), and a final select returns x itself for +-0 and +inf.  For x
+// in [2^-767, DBL_MAX] neither repair changes anything, so the bare chain gives the same bits (tests/test_kat.py::
+// test_fast_sqrt_div_bit_identical); any other x (zero, negative, tiny, inf, NaN) takes sqrt() on an exec-masked cold
+// path.  Saves the scaling compare/ldexp pair and the zero/inf select (~7 VALU) per call.
+#ifndef SHUD_SQRT_NR
+#define SHUD_SQRT_NR 0
 #endif
+__device__ __forceinline__ double sqrt_nr(double x) {
+#if SHUD_SQRT_NR
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = y * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    h = __builtin_fma(h, r, h);
+    g = __builtin_fma(g, r, g);
+    double d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    if (__builtin_expect(!(x >= 0x1p-767 && x <= 0x1.fffffffffffffp+1023), 0)) g = sqrt(x);
+    return g;
+#else
+    return sqrt(x);
+#endif
+}
+// division: LLVM's lowering is r = rcp(b') refined by two Newton steps, q = a' r, e = fma(-b', q, a'), q + e r (as
+// v_div_fmas), then v_div_fixup for special operands, where v_div_scale rescales a, b (a' , b') only when 1/b, a/b or a
+// would leave the normal range.  For |b| in [2^-100, 2^100] and |a| in [2^-900, 2^600] no operand is rescaled and
+// the fixup returns the quotient as is, so the bare chain gives the same bits; and r depends on b alone, so two
+// divisions by one divisor share it (Recip).  Other operands take the IEEE division on an exec-masked cold path.
+#ifndef SHUD_DIV_NR
+#define SHUD_DIV_NR 0
+#endif
+struct Recip {
+    double b, r;
+    bool ok;                 // |b| in [2^-100, 2^100]
+};
+__device__ __forceinline__ Recip recip_nr(double b) {
+    Recip R;
+    R.b = b;
+#if SHUD_DIV_NR
+    double r = __builtin_amdgcn_rcp(b);
+    double e = __builtin_fma(-b, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-b, r, 1.0);
+    R.r = __builtin_fma(r, e, r);
+    const double bb = __builtin_fabs(b);
+    R.ok = bb >= 0x1p-100 && bb <= 0x1p100;
+#else
+    R.r = 0.;
+    R.ok = false;
+#endif
+    return R;
+}
+__device__ __forceinline__ double div_nr(double a, const Recip &R) {
+#if SHUD_DIV_NR
+    const double q0 = a * R.r;
+    const double e = __builtin_fma(-R.b, q0, a);
+    double q = __builtin_fma(e, R.r, q0);
+    const double aa = __builtin_fabs(a);
+    if (__builtin_expect(!(R.ok && aa >= 0x1p-900 && aa <= 0x1p600), 0)) q = a / R.b;
+    return q;
+#else
+    return a / R.b;
+#endif
+}
 
 // ---- constants: src/Model/Macros.hpp:46-77 ----
 #define K_EPSILON 0.005
@@ -82,7 +110,50 @@ __device__ __forceinline__ double cdiv(double a, double b, double rb) {
 // functions.hpp:117-123 (NOT fmin/fmax: NaN behaviour must match)
 __device__ __forceinline__ double rmin(double a, double b) { return (a > b ? b : a); }
 __device__ __forceinline__ double rmax(double a, double b) { return (a < b ? b : a); }
-__device__ __forceinline__ double pow23(double x) { double t = SCBRT(x); return t * t; }
+// glibc's cbrt (sysdeps/ieee754/dbl-64/s_cbrt.c, glibc 2.35: the reference's libm for pow23's cbrt,
+// Equations.hpp:36-39) restated operation for operation: x = xm 2^xe with xm in [0.5, 1), a degree-6 polynomial u ~
+// xm^(1/3), one Halley step u (u^3 + 2 xm) / (2 u^3 + xm), times 2^((xe mod 3) / 3) from a 5-entry table, scaled by
+// 2^(xe / 3).  2 xm and 2 u^3 are exact, so t2 + 2 xm and 2 t2 + xm are single fmas with the same rounding; the Halley
+// quotient has numerator and denominator in [0.7, 3], where the bare division chain (div_nr's, without v_div_scale /
+// v_div_fixup) is the IEEE quotient.  Zero, infinite and NaN x return x + x, as glibc does.  Bit-identical to glibc's
+// cbrt (tests/test_kat.py::test_cbrt_glibc_bit_identical), so Manning's R^(2/3) is the oracle's bit for bit.
+#ifndef SHUD_CBRT_GLIBC
+#define SHUD_CBRT_GLIBC 0
+#endif
+__device__ __forceinline__ double cbrt_glibc(double x) {
+    constexpr double kC2 = 1.2599210498948731648, kSqC2 = 1.5874010519681994748;   // 2^(1/3), 2^(2/3)
+    int xe;
+    const double xm = __builtin_frexp(__builtin_fabs(x), &xe);
+    double p = 0.784932344976639262 - 0.145263899385486377 * xm;
+    p = -1.83469277483613086 + p * xm;
+    p = 2.44693122563534430 + p * xm;
+    p = -2.11499494167371287 + p * xm;
+    p = 1.50819193781584896 + p * xm;
+    const double u = 0.354895765043919860 + p * xm;
+    const double t2 = u * u * u;
+    const double num = u * __builtin_fma(xm, 2.0, t2), den = __builtin_fma(t2, 2.0, xm);
+    double r = __builtin_amdgcn_rcp(den);                       // num / den: the division chain, no repairs
+    double e = __builtin_fma(-den, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-den, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    double q = num * r;
+    e = __builtin_fma(-den, q, num);
+    q = __builtin_fma(e, r, q);
+    const int q3 = xe / 3, rem = xe - 3 * q3;                   // C's truncating / and %
+    const double f = rem == 0 ? 1.0 : rem == 1 ? kC2 : rem == 2 ? kSqC2 : rem == -1 ? 1.0 / kC2 : 1.0 / kSqC2;
+    const double ym = q * f;
+    const double res = __builtin_ldexp(x > 0.0 ? ym : -ym, q3);
+    return __builtin_isfpclass(x, 0x0003 | 0x0204 | 0x0060) ? x + x : res;    // NaN, +-inf, +-0
+}
+__device__ __forceinline__ double pow23(double x) {
+#if SHUD_CBRT_GLIBC
+    const double t = cbrt_glibc(x);
+#else
+    const double t = cbrt(x);
+#endif
+    return t * t;
+}
 
 // Equations.hpp:54-63.  The reference's two branches differ only in the sqrt argument (S or -S) and a leading
 // -1.0 factor; IEEE multiplication and division round sign-symmetrically, so (-1.0*x)*A*p/n == -(x*A*p/n) bit
@@ -90,20 +161,16 @@ __device__ __forceinline__ double pow23(double x) { double t = SCBRT(x); return 
 // the compiler if-converted the two branches into two full sqrt sequences per call otherwise.
 __device__ __forceinline__ double manning(double A, double n, double R, double S) {
     const bool pos = S > 0;
-    const double t = SDIV(SSQRT(pos ? S : -S) * A * pow23(R), n);
+    const double t = sqrt_nr(pos ? S : -S) * A * pow23(R) / n;
     return pos ? t : -t;
 }
 // Equations.cpp:116-134 (range check reported by the caller).  The two macropore branches divide different
 // numerators by different divisors; the numerator and divisor are selected per branch and ONE division follows
 // the join, so a wave whose lanes take both branches runs one division sequence instead of two (same operations
-// per lane, same bits).  SHUD_EKH1=0: the branch-local divisions (A/B).
-#ifndef SHUD_EKH1
-#define SHUD_EKH1 1
-#endif
+// per lane, same bits).
 __device__ __forceinline__ double eff_kh(double ygw, double aq, double macd, double kmac, double af,
                                          double kmx) {
     double e;
-#if SHUD_EKH1
     if (macd <= K_ZERO || ygw < aq - macd) e = kmx;
     else {
         double num, den;
@@ -113,13 +180,8 @@ __device__ __forceinline__ double eff_kh(double ygw, double aq, double macd, dou
             num = kmac * t * af + kmx * (aq - macd + t * (1 - af));
             den = ygw;
         }
-        e = SDIV(num, den);
+        e = num / den;
     }
-#else
-    if (macd <= K_ZERO || ygw < aq - macd) e = kmx;
-    else if (ygw > aq) e = SDIV(kmac * macd * af + kmx * (aq - macd * af), aq);
-    else e = SDIV(kmac * (ygw - (aq - macd)) * af + kmx * (aq - macd + (ygw - (aq - macd)) * (1 - af)), ygw);
-#endif
     return e;
 }
 // MD_RiverFlux.cpp:65-98
@@ -133,14 +195,12 @@ __device__ __forceinline__ double weir_jtoi(double zi, double yi, double zj, dou
     double y = hi - zbank;
     const bool on = up ? ((y > 0.) & (yj > thr)) : (y > 0. && yi > thr);
     if (up ? (hi > zbank) : (hj > zbank)) y = up ? dh : -dh;
-    const double t = cwr * SSQRT(2. * K_GRAV * y) * width * y * 60.;
+    const double t = cwr * sqrt_nr(2. * K_GRAV * y) * width * y * 60.;
     return on ? (up ? t : -t) : 0.;
 }
 // Flux_RiverElement.cpp:11-55
-// RD: D's correctly rounded reciprocal rD is given (cdiv); otherwise the plain division
-template <bool RD = false>
-__device__ __forceinline__ double r2e_gw(double yr, double zr, double ye, double ze, double kele,
-                                         double kriv, double L, double D, double rD = 0.) {
+__device__ __forceinline__ double r2e_gw(double yr, double zr, double ye, double ze, double kele, double kriv,
+                                         double L, double D) {
     if (kele < K_ZERO || kriv < K_ZERO) return 0.;
     double K = (kele * 1. + kriv * 1.) / (1. + 1.);   // meanArithmetic(k1,k2,1,1) Equations.hpp:50-52
     // both flowing branches evaluate A * K * (dh / D) on their own A: one division, branch-selected A
@@ -148,37 +208,12 @@ __device__ __forceinline__ double r2e_gw(double yr, double zr, double ye, double
     const bool in = dh > K_ZERO;
     const double A = (in && !(he > zr)) ? yr * L : (yr + (he - zr)) * .5 * L;
     const bool on = in ? !(yr < K_EPSILON) : (dh < -K_ZERO && ye > K_ZERO);
-    return on ? A * K * (RD ? CDIV_(dh, D, rD) : SDIV(dh, D)) : 0.;
+    return on ? A * K * (dh / D) : 0.;
 }
 // x / a for x = 0.0 (QSS, never assigned by the reference): +-0 with a's sign for a non-zero a, NaN for a zero
 // or NaN a — the IEEE quotient, without a division
 __device__ __forceinline__ double zero_over(double a) {
     return (a != 0. && a == a) ? __builtin_copysign(0.0, a) : __builtin_nan("");
-}
-
-// single-use stream loads: non-temporal when the variant asks for it (VAR bit 1)
-template <int VAR, class T>
-__device__ __forceinline__ T ld1(const T *p) {
-    if (VAR & 2) return __builtin_nontemporal_load(p);
-    return *p;
-}
-template <int VAR, class T>
-__device__ __forceinline__ void st1(T *p, T v) {
-    if (VAR & 2) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
-// minimum waves per SIMD requested by the variant (VAR bits 2-3)
-template <int VAR> struct LB { static constexpr int w = ((VAR >> 2) & 3) == 1 ? 6 : ((VAR >> 2) & 3) == 2 ? 8 : 1; };
-// workgroup -> element block: VAR bit 0 deals consecutive element blocks to the same XCD (blocks are
-// dispatched round-robin over the 8 XCDs, so b and b+8 share an L2): the rows above/below an element
-// block then sit in that XCD's L2.  Placement affects speed only, never results.
-template <int VAR>
-__device__ __forceinline__ int block_id() {
-    if (VAR & 1) {
-        const int per = gridDim.x >> 3;            // grid is padded to a multiple of 8 by the launcher
-        return (blockIdx.x & 7) * per + (blockIdx.x >> 3);
-    }
-    return blockIdx.x;
 }
 
 struct RivGeom { double csarea, csperem, topw, toparea; };
@@ -197,55 +232,15 @@ __device__ __forceinline__ RivGeom riv_geom(double w0, double bs, double len, do
     g.toparea = (ta < 0.) ? 0. : ta;
     return g;
 }
-// pow(x, y) for a positive finite base and a finite exponent whose product y*ln(x) cannot overflow: OCML's
-// own pow core (__ocml_pow_f64, ocml.bc: extended-precision log, the two-product, extended exp) without the
-// ~30 selects that handle negative/zero/infinite/NaN bases, integer exponents and infinities.  On that domain
-// every special-case select of __ocml_pow_f64 passes the core's value through, so the result is the same
-// bits (tests/test_kat.py::test_pow_pos_bit_identical); x = 1 gives exp(y*0) = 1 exactly, as pow does.
-typedef double shud_v2d __attribute__((ext_vector_type(2)));
-extern "C" __device__ shud_v2d __ocmlpriv_epln_f64(double);
-extern "C" __device__ double __ocmlpriv_expep_f64(shud_v2d);
-__device__ __forceinline__ double pow_pos(double x, double y) {
-    const shud_v2d l = __ocmlpriv_epln_f64(x);          // ln x = l.y + l.x (head, tail)
-    const double hi = y * l.y;
-    const double lo = __builtin_fma(y, l.x, __builtin_fma(y, l.y, -hi));
-    const double s = hi + lo;
-    shud_v2d a;
-    a.y = s;
-    a.x = lo - (s - hi);
-    return __ocmlpriv_expep_f64(a);
-}
-#ifndef SHUD_POWPOS
-#define SHUD_POWPOS 1
-#endif
-// satKfun's pow: shud_pow_tab (shud_powtab.h, default: table-driven log/exp, ~60 VALU, within 0.66 ulp of x^y and
-// equal to glibc's pow on 99.9 % of satKfun's domain — tests/test_kat.py); SHUD_POWTAB=0: pow_pos (OCML's pow core,
-// ~180 VALU, the device pow's bits)
-#ifndef SHUD_POWTAB
-#define SHUD_POWTAB 1
-#endif
-#if SHUD_ABL & 1
-#define SPOW_SAT(a, b) SPOW(a, b)
-#elif SHUD_POWTAB
-#define SPOW_SAT(a, b) shud_pow_tab(a, b)
-#elif SHUD_POWPOS
-#define SPOW_SAT(a, b) pow_pos(a, b)
-#else
-#define SPOW_SAT(a, b) SPOW(a, b)
-#endif
-
 // satKfun, Equations.cpp:136-141, with the class exponents ex1 = n/(n-1), ex2 = (n-1)/n precomputed.
 // Both bases are positive here: satn in (ZERO, 0.99] (the callers' clamps), 1 - satn^ex1 in (0, 1];
-// exponents are class constants of Beta > 1 (checked by the handle).  lt / et: pow_tab's log / exp tables (the element
-// kernel passes its LDS copy; default: __constant__ memory)
+// exponents are class constants of Beta > 1 (checked by the handle; the SoA kernel takes the full pow otherwise).
+// pow is shud_pow_tab (shud_powtab.h: table-driven log/exp, ~60 VALU, within 0.51 ulp of x^y and equal to glibc's pow
+// on 99.93 % of satKfun's domain, tests/test_kat.py).  lt / et: its log / exp tables (the packed element kernel passes
+// its LDS copy; default: __constant__ memory)
 __device__ __forceinline__ double sat_kfun(double satn, double ex1, double ex2, const double *lt, const double *et) {
-#if SHUD_POWTAB && !(SHUD_ABL & 1)
     const double tmp = -1. + shud_pow_tab_t(1. - shud_pow_tab_t(satn, ex1, lt, et), ex2, lt, et);
-#else
-    (void)lt; (void)et;
-    const double tmp = -1. + SPOW_SAT(1. - SPOW_SAT(satn, ex1), ex2);
-#endif
-    return SSQRT(satn) * tmp * tmp;
+    return sqrt_nr(satn) * tmp * tmp;
 }
 __device__ __forceinline__ double sat_kfun(double satn, double ex1, double ex2) {
     return sat_kfun(satn, ex1, ex2, SHUD_PT_LOGTAB, shud_pt_exptab);
@@ -257,25 +252,15 @@ __device__ __forceinline__ double sat_kfun(double satn, double ex1, double ex2) 
 // OCML's cos (__ocml_cos_f64: |x|, trigred = small or Payne-Hanek reduction by |x| < 2^30, sincosred2, quadrant
 // selects, a non-finite select) reduces to its small-argument path; cos_small calls that path's own pieces in the
 // same order and returns the same bits (tests/test_kat.py::test_cos_small_bit_identical) without the large-argument
-// branch and the |x| / finiteness selects.  SHUD_COS_SMALL=0: OCML's cos (A/B).
-#ifndef SHUD_COS_SMALL
-#define SHUD_COS_SMALL 1
-#endif
+// branch and the |x| / finiteness selects.
 // fma(a, b, c) for a constant addend c: v_fma_f64 with c in an SGPR pair (one VALU + two SALU moves), where the
 // compiler's v_fmac_f64 form needs c in a VGPR pair (two v_mov_b32 + the fmac: three VALU).  Same operation, same
 // bits.  cos_small's nine constant-addend steps: -14 static VALU; element kernel 0.6017 vs 0.6012 ms, wall per eval
-// 0.578 vs 0.580 ms (within noise, profiles/r05/tiles2/).  SHUD_FMA_SC=0: __builtin_fma (A/B).
-#ifndef SHUD_FMA_SC
-#define SHUD_FMA_SC 1
-#endif
+// 0.578 vs 0.580 ms (within noise, profiles/r05/tiles2/).
 __device__ __forceinline__ double fma_sc(double a, double b, double c) {
-#if SHUD_FMA_SC
     double r;
     asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
     return r;
-#else
-    return __builtin_fma(a, b, c);
-#endif
 }
 // OCML's __ocmlpriv_trigredsmall_f64 + __ocmlpriv_sincosred2_f64 (ocml.bc, ROCm 7.2) restated operation for
 // operation (their results come back in registers; a call to the bitcode's struct-returning functions went through
@@ -316,14 +301,9 @@ __device__ __forceinline__ double cos_small(double x) {            // 0 <= x < 2
     const double c = (qi & 1) ? -sn : cs;
     return qi > 1 ? -c : c;
 }
-#if SHUD_COS_SMALL && !(SHUD_ABL & 2)
-#define SCOS_PI(a) cos_small(a)
-#else
-#define SCOS_PI(a) SCOS(a)
-#endif
 __device__ __forceinline__ double soil_moisture_stress(double b) {
     b = rmin(rmax(0., b), 1.);
-    return 0.5 * (1 - SCOS_PI(K_PI * b));
+    return 0.5 * (1 - cos_small(K_PI * b));
 }
 // fun_dAtodY + Quadratic, functions.hpp:125-153
 __device__ __forceinline__ double da_to_dy(double dA, double w_top, double s) {

@@ -55,6 +55,25 @@ int shud_fail(int code, const char *fmt, ...) {
     return code;
 }
 
+// Run-time switches read from the environment (A/B measurements and tests).  Each is parsed strictly: a value that is
+// not an integer in [lo, hi] is ignored with a warning, and a value that takes effect is announced once per process on
+// stderr — a stray variable in a user's environment cannot silently change kernel selection.
+static int env_knob(const char *name, int def, int lo, int hi) {
+    const char *v = getenv(name);
+    if (!v || !*v) return def;
+    char *end = nullptr;
+    const long x = strtol(v, &end, 10);
+    static std::vector<std::string> said;
+    const bool first = std::find(said.begin(), said.end(), std::string(name)) == said.end();
+    if (first) said.push_back(name);
+    if (*end || x < lo || x > hi) {
+        if (first) fprintf(stderr, "shud_rhs: ignoring %s=%s (expected an integer in [%d, %d])\n", name, v, lo, hi);
+        return def;
+    }
+    if (first && x != def) fprintf(stderr, "shud_rhs: %s=%ld in effect (default %d)\n", name, x, def);
+    return (int)x;
+}
+
 int shud_reset_err(shud_rhs *h) {
     DevErr z{};
     z.flags = 0;
@@ -92,6 +111,8 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
                         const std::vector<int> &up_idx);
 
 static int build_lakes(shud_rhs *h, const ShudMeshSoA *m, const ShudPartition *part);
+static int build_river_fold(shud_rhs *h, const ShudMeshSoA *m, const std::vector<int> &up_off,
+                            const std::vector<int> &up_idx);
 static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, const ShudRhsOptions *opt,
                  const ShudPartition *part) {
     const int NE = m->num_ele, NR = m->num_riv, NS = m->num_seg;
@@ -105,7 +126,6 @@ static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, cons
     h->n_own = part ? part->n_own_ele : NE;
     h->n_segghost = part ? part->n_segghost_ele : 0;
     h->n_own_riv = part ? part->n_own_riv : NR;
-    if (const char *v = getenv("SHUD_RHS_ELE_VARIANT")) h->variant = atoi(v);
     if (h->n_own < 0 || h->n_own + h->n_segghost > NE || h->n_own_riv < 0 || h->n_own_riv > NR)
         return shud_fail(SHUD_ERR_ARG, "partition counts inconsistent with mesh sizes");
 
@@ -326,6 +346,7 @@ static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, cons
 #undef UP
     if ((rc = build_packed(h, m, p, eflags, seg_off, up_off, up_idx))) return rc;
     if (h->lakeon && (rc = build_lakes(h, m, part))) return rc;
+    if (!part && (rc = build_river_fold(h, m, up_off, up_idx))) return rc;
     if ((rc = h->dalloc(&h->d_err, 1))) return rc;
     if ((rc = h->dalloc(&h->d_warn, (size_t)kWarnSlots * kWarnStride))) return rc;
     d.err = h->d_err;
@@ -345,8 +366,7 @@ static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, cons
 static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, const std::vector<int> &eflags,
                         const std::vector<int> &seg_off, const std::vector<int> &up_off,
                         const std::vector<int> &up_idx) {
-    const char *env = getenv("SHUD_RHS_PACKED");
-    if ((env && env[0] == '0') || h->variant) return 0;
+    if (!env_knob("SHUD_RHS_PACKED", 1, 0, 1)) return 0;         // 0: the SoA kernel (tests, A/B)
     const int NE = m->num_ele;
     if (!m->rough || NE == 0) return 0;
     // avgRough must be the reference's 0.5*(Rough_i + Rough_nabr) / Rough_i (Element.cpp:249-265).  Owned
@@ -428,13 +448,13 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     // class constant depends on them; Sy's reciprocal is replaced by the IEEE division, the same bits).
     // SHUD_RHS_HYB=0: off (A/B); =2: KsatH streamed even when the classes fit (timing the hybrid path on any model).
     uint32_t hmask = 0;
-    if (const char *hf = getenv("SHUD_RHS_HYB"); hf && hf[0] == '2' && !h->lakeon) {
+    const int hyb = env_knob("SHUD_RHS_HYB", 1, 0, 2);
+    if (hyb == 2 && !h->lakeon) {
         hmask = 1u << CF_KsatH;
     } else {
-        const char *hy = getenv("SHUD_RHS_HYB");
         const uint32_t streamable = 1u << CF_macD | 1u << CF_macKsatH | 1u << CF_vAreaF | 1u << CF_KsatH |
                                     1u << CF_KsatV | 1u << CF_Sy | 1u << CF_RzD | 1u << CF_depression | 1u << CF_rough;
-        if (!h->lakeon && !(hy && hy[0] == '0') && (!fits || (int)table.size() > kLdsClassMax) &&
+        if (!h->lakeon && hyb != 0 && (!fits || (int)table.size() > kLdsClassMax) &&
             count_tuples(streamable, kLdsClassMax) <= kLdsClassMax) {
             // base classes: the tuples of the fields that cannot be streamed; then, per streamable field, how many
             // (base class, value) pairs it makes — the fields that split the base classes most are streamed first
@@ -484,10 +504,10 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     // with 33 classes in LDS; from L2 0.83 ms at 132 classes, 1.21 at 495, 1.49 at 1,980, 1.66 at 13,200; the
     // SoA kernel 1.09 ms at any count -> SoA above 600 (SHUD_RHS_L2_CLASS=1 forces the L2 table at any count and
     // disables the 1024-thread LDS kernel, =0 forces SoA above 128: A/B and bench.py many_class)
-    const char *l2 = getenv("SHUD_RHS_L2_CLASS");
-    const int l2_max = (l2 && l2[0] == '1') ? 32768 : (l2 && l2[0] == '0') ? kLdsClassMax : kLdsClassMaxBig;
+    const int l2 = env_knob("SHUD_RHS_L2_CLASS", -1, 0, 1);
+    const int l2_max = l2 == 1 ? 32768 : l2 == 0 ? kLdsClassMax : kLdsClassMaxBig;
     if (ncls > l2_max) return 0;
-    h->dp.lds_big = (l2 && l2[0] == '1') ? 0 : 1;
+    h->dp.lds_big = l2 == 1 ? 0 : 1;
     std::vector<double> ctab((size_t)CF_STRIDE * ncls, 0.0);
     for (int c = 0; c < ncls; c++) {
         std::vector<double> &t = table[c];
@@ -497,8 +517,8 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         t[CF_dTh] = t[CF_ThetaS] - t[CF_ThetaR];
         t[CF_ex1] = t[CF_Beta] / (t[CF_Beta] - 1.);
         t[CF_ex2] = (t[CF_Beta] - 1.) / t[CF_Beta];
-        // the packed kernel's satKfun uses pow_pos (positive bases, finite exponents: shud_physics.h);
-        // any other Beta keeps the SoA layout, whose kernel calls the full pow
+        // the packed kernel's satKfun uses pow_tab (positive bases, finite exponents: shud_physics.h);
+        // any other Beta keeps the SoA layout, whose kernel calls the full pow for it
         if (!(t[CF_Beta] > 1.) || !std::isfinite(t[CF_ex1]) || !std::isfinite(t[CF_ex2])) return 0;
         t[CF_pj] = 1. - t[CF_ImpAF];
         t[CF_omh] = 1. - t[CF_hAreaF];
@@ -570,76 +590,28 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
         P.hnb = (hmask & (1u << CF_macD | 1u << CF_macKsatH | 1u << CF_vAreaF | 1u << CF_KsatH | 1u << CF_rough)) != 0;
     } P.meta = meta_d; P.ged = ged_d; P.area = area_d;
     P.seg_first = sf_d;
-    // host reciprocals of static geometric divisors for a kernel built with SHUD_RCP (A/B builds)
-    const int rcp = shud_ele_rcp_mask();
-    if (rcp & 1) {
-        std::vector<double> ra(NE);
-        for (int i = 0; i < NE; i++) {
-            if (!cdiv_divisor_ok(m->area[i])) return 0;
-            ra[i] = 1. / m->area[i];
-        }
-        double *ra_d;
-        if ((rc = h->upload(&ra_d, ra.data(), NE))) return rc;
-        P.r_area = ra_d;
-    }
-    if (rcp & 2) {
-        std::vector<double> rd(3 * (size_t)NE);
-        for (size_t k = 0; k < rd.size(); k++) {
-            const double d = m->dist2nabor[k];
-            if (m->nabr[k] >= 0 && !cdiv_divisor_ok(d)) return 0;      // used on interior and bank edges only
-            rd[k] = 1. / d;
-        }
-        double *rd_d;
-        if ((rc = h->upload(&rd_d, rd.data(), rd.size()))) return rc;
-        P.r_d2n = rd_d;
-    }
-    {   // element-sorted segment records with their reach's statics (seg_perm: element-sorted -> reference)
-        const int NSg = m->num_seg;
-        std::vector<double2> lc(NSg), dk(NSg);
-        std::vector<int2> rb(NSg);
-        std::vector<double> bt(NSg);
+    {   // element-sorted segments {length, Cwr} + their reach; one 32-B record per reach with the statics the segment
+        // fluxes read (seg_perm: element-sorted -> reference)
+        const int NSg = m->num_seg, NRl = m->num_riv;
+        std::vector<double2> lc(NSg), rr(2 * (size_t)NRl);
+        std::vector<int> sr(NSg);
         for (int k = 0; k < NSg; k++) {
-            const int s = h->seg_perm[k], r = m->seg_riv[s];
+            const int s = h->seg_perm[k];
             lc[k] = make_double2(m->seg_length[s], m->seg_cwr[s]);
-            dk[k] = make_double2(m->riv_depth[r], m->riv_ksath[r]);
-            rb[k] = make_int2(r, m->riv_bc ? m->riv_bc[r] : 0);
-            bt[k] = m->riv_bedthick[r];
+            sr[k] = m->seg_riv[s];
         }
-        double2 *lc_d, *dk_d; int2 *rb_d; double *bt_d;
+        for (int r = 0; r < NRl; r++) {
+            const int32_t two[2] = {m->riv_bc ? m->riv_bc[r] : 0, 0};
+            double bits;
+            memcpy(&bits, two, sizeof bits);
+            rr[2 * (size_t)r] = make_double2(m->riv_depth[r], m->riv_ksath[r]);
+            rr[2 * (size_t)r + 1] = make_double2(m->riv_bedthick[r], bits);
+        }
+        double2 *lc_d, *rr_d; int *sr_d;
         if ((rc = h->upload(&lc_d, lc.data(), NSg))) return rc;
-        P.sg_lc = lc_d;
-        if (shud_ele_seg_rrec()) {                     // segments -> per-reach records (shud_dev.h sg_r / rrec)
-            const int NRl = m->num_riv;
-            std::vector<int> sr(NSg);
-            std::vector<double2> rr(2 * (size_t)NRl);
-            for (int k = 0; k < NSg; k++) sr[k] = rb[k].x;
-            for (int r = 0; r < NRl; r++) {
-                const int32_t two[2] = {m->riv_bc ? m->riv_bc[r] : 0, 0};
-                double bits;
-                memcpy(&bits, two, sizeof bits);
-                rr[2 * (size_t)r] = make_double2(m->riv_depth[r], m->riv_ksath[r]);
-                rr[2 * (size_t)r + 1] = make_double2(m->riv_bedthick[r], bits);
-            }
-            int *sr_d; double2 *rr_d;
-            if ((rc = h->upload(&sr_d, sr.data(), NSg))) return rc;
-            if ((rc = h->upload(&rr_d, rr.data(), rr.size()))) return rc;
-            P.sg_r = sr_d; P.rrec = rr_d;
-        } else {
-            if ((rc = h->upload(&dk_d, dk.data(), NSg))) return rc;
-            if ((rc = h->upload(&rb_d, rb.data(), NSg))) return rc;
-            if ((rc = h->upload(&bt_d, bt.data(), NSg))) return rc;
-            P.sg_dk = dk_d; P.sg_rb = rb_d; P.sg_bt = bt_d;
-        }
-        if (rcp & 4) {
-            std::vector<double> rbt(NSg);
-            for (int k = 0; k < NSg; k++) {
-                if (!cdiv_divisor_ok(bt[k])) return 0;
-                rbt[k] = 1. / bt[k];
-            }
-            double *rbt_d;
-            if ((rc = h->upload(&rbt_d, rbt.data(), NSg))) return rc;
-            P.sg_rbt = rbt_d;
-        }
+        if ((rc = h->upload(&sr_d, sr.data(), NSg))) return rc;
+        if ((rc = h->upload(&rr_d, rr.data(), rr.size()))) return rc;
+        P.sg_lc = lc_d; P.sg_r = sr_d; P.rrec = rr_d;
         if ((rc = h->upload(&P.qseg2, (const double2 *)nullptr, NSg))) return rc;
     }
     if ((rc = h->upload(&P.s_np, (const double2 *)nullptr, NE))) return rc;
@@ -657,17 +629,6 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     std::vector<int> rstart(NR, 0), rcnt(NR, 0);
     for (int q = NS - 1; q >= 0; q--) rstart[m->seg_riv[rorder[q]]] = q;
     for (int s = 0; s < NS; s++) rcnt[m->seg_riv[s]]++;
-    // SHUD_RHS_SEG_ORDER=reach (A/B): the element kernel scatters each segment's flux pair to its reach-sorted
-    // slot and the river kernel reads its segments contiguously; default: element order + gathers
-    if (const char *so = getenv("SHUD_RHS_SEG_ORDER"); so && !strcmp(so, "reach") && !h->partitioned) {
-        std::vector<int> rpos_of(NS), rpos(NS);
-        for (int q = 0; q < NS; q++) rpos_of[rorder[q]] = q;
-        for (int k = 0; k < NS; k++) rpos[k] = rpos_of[h->seg_perm[k]];
-        int *rp_d;
-        if ((rc = h->upload(&rp_d, rpos.data(), NS))) return rc;
-        P.seg_rpos = rp_d;
-        h->rseg_perm = rorder;
-    }
     std::vector<double2> rv(4 * (size_t)NR);
     std::vector<int4> ru(NR);
     const int nor = h->n_own_riv;
@@ -695,16 +656,83 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     if ((rc = h->upload(&ru_d, ru.data(), NR))) return rc;
     P.rv = rv_d; P.rv_u = ru_d;
     P.riv_sb = choose_riv_sb(rcnt.data(), nor);
-    if (const char *sb = getenv("SHUD_RIV_SB"); sb && (atoi(sb) == 6 || atoi(sb) == 8)) P.riv_sb = atoi(sb);   // tests
-    // QrivDown pre-pass slots (shud_dev.h DevPacked::qdown); SHUD_RHS_QD=0: the river kernel recomputes (A/B)
-    if (NR > 0 && !(getenv("SHUD_RHS_QD") && getenv("SHUD_RHS_QD")[0] == '0')) {
+    if (const int sb = env_knob("SHUD_RIV_SB", 0, 6, 8); sb == 6 || sb == 8) P.riv_sb = sb;   // tests: both batch sizes
+    // QrivDown pre-pass slots (shud_dev.h DevPacked::qdown); SHUD_RHS_QD=0: the river kernel recomputes (tests, A/B)
+    if (NR > 0 && env_knob("SHUD_RHS_QD", 1, 0, 1)) {
         if ((rc = h->upload(&P.qdown, (const double *)nullptr, NR))) return rc;
         P.nqd = NR;
     }
-    P.qd_pm = getenv("SHUD_QD_POS") ? atoi(getenv("SHUD_QD_POS")) : 1000;
-    P.qd_pm_fold = getenv("SHUD_QD_POS_FOLD") ? atoi(getenv("SHUD_QD_POS_FOLD")) : 1000;
+    P.qd_pm = env_knob("SHUD_QD_POS", 1000, 0, 1000);
+    P.qd_pm_fold = env_knob("SHUD_QD_POS_FOLD", 1000, 0, 1000);
     h->n_classes = ncls;
     h->packed = true;
+    return 0;
+}
+
+// River fold (DevPacked::rf_*, shud_ele_packed.hip shud_rhs_kernel_packed_rf): the reaches ride in the last blocks of
+// the element launch.  Per reach tile (256 reaches, the river kernel's tiles): the element tiles owning any segment of
+// every 128-B qseg2 line its segment gathers touch (whole lines: no reach tile ever caches a line another element tile
+// has yet to write), and the QrivDown blocks of its own and upstream reaches — each a contiguous range (band-numbered
+// meshes: syn-10M spans <= 99 element tiles and <= 11 QrivDown blocks).  River blocks are dealt to reach tiles in the
+// order their inputs come due: by the latest launch block among those they wait for.  Unpartitioned, lake-free
+// handles on the LDS class table only; SHUD_RHS_RFOLD=1 (measured slower so far, DESIGN §4 round 6: opt-in).
+static int build_river_fold(shud_rhs *h, const ShudMeshSoA *m, const std::vector<int> &up_off,
+                            const std::vector<int> &up_idx) {
+    DevPacked &P = h->dp;
+    const int nor = h->n_own_riv, NS = m->num_seg, n = h->n_own + h->n_segghost;
+    if (!h->packed || h->lakeon || h->partitioned || nor <= 0 || !P.qdown || P.nqd <= 0 || P.nh ||
+        P.ncls > kLdsClassMax || !env_knob("SHUD_RHS_RFOLD", 0, 0, 1))
+        return 0;
+    P.rf_qd_pm = env_knob("SHUD_QD_POS_RF", 0, 0, 1000);
+    const EleGrid g = ele_grid(n, P.nqd, P.rf_qd_pm);
+    const int ntile = (nor + 255) / 256, nl = (NS + 7) / 8;
+    // element tile range of every 128-B line of qseg2 (element-sorted positions, 8 per line)
+    std::vector<int> lmin(nl, INT_MAX), lmax(nl, -1), pos_of(NS);
+    for (int k = 0; k < NS; k++) {
+        const int t = m->seg_ele[h->seg_perm[k]] / 256;
+        pos_of[h->seg_perm[k]] = k;
+        lmin[k / 8] = std::min(lmin[k / 8], t);
+        lmax[k / 8] = std::max(lmax[k / 8], t);
+    }
+    std::vector<int4> dep(ntile);
+    for (int j = 0; j < ntile; j++) dep[j] = make_int4(INT_MAX, -1, j, j);   // own reaches: QrivDown block j
+    for (int s = 0; s < NS; s++) {
+        const int r = m->seg_riv[s];
+        if (r >= nor) continue;
+        const int l = pos_of[s] / 8;
+        int4 &d = dep[r / 256];
+        d.x = std::min(d.x, lmin[l]);
+        d.y = std::max(d.y, lmax[l]);
+    }
+    for (int r = 0; r < nor; r++)
+        for (int k = up_off[r]; k < up_off[r + 1]; k++) {
+            int4 &d = dep[r / 256];
+            d.z = std::min(d.z, up_idx[k] / 256);
+            d.w = std::max(d.w, up_idx[k] / 256);
+        }
+    std::vector<std::pair<long long, int>> due(ntile);
+    for (int j = 0; j < ntile; j++) {
+        int4 &d = dep[j];
+        if (d.y < 0) { d.x = 0; d.y = -1; }                  // no segments: QrivDown blocks only
+        long long key = -1;
+        for (int t = d.x; t <= d.y; t++) key = std::max<long long>(key, g.block_of_tile(t));
+        for (int q = d.z; q <= d.w; q++) key = std::max<long long>(key, g.block_of_qd(q));
+        due[j] = {key, j};
+    }
+    std::stable_sort(due.begin(), due.end());
+    std::vector<int> order(ntile);
+    for (int j = 0; j < ntile; j++) order[j] = due[j].second;
+    int rc;
+    unsigned *flag_d; int *tile_d; int4 *dep_d;
+    if ((rc = h->upload(&flag_d, (const unsigned *)nullptr, (size_t)g.nb_e + g.nb_q))) return rc;
+    if ((rc = h->upload(&tile_d, order.data(), ntile))) return rc;
+    if ((rc = h->upload(&dep_d, dep.data(), ntile))) return rc;
+    P.rf_flag = flag_d; P.rf_tile = tile_d; P.rf_dep = dep_d; P.rf_ntile = ntile;
+    h->rf_epoch = 0;
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device) == hipSuccess && khz > 0)
+        h->wall_khz = khz;
+    h->rf_timeout = (unsigned long long)(env_knob("SHUD_HALO_TIMEOUT_MS", 5000, 1, 3600000) * h->wall_khz);
     return 0;
 }
 
@@ -712,7 +740,7 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
 static int build_lakes(shud_rhs *h, const ShudMeshSoA *m, const ShudPartition *part) {
     const int NE = m->num_ele, NR = m->num_riv, NL = h->NL;
     const int NO = h->n_own;                   // lake and bank elements are owned (partition plan)
-    if (!h->packed || h->variant)
+    if (!h->packed)
         return shud_fail(SHUD_ERR_UNSUPPORTED, "lakes need the packed layout (mesh did not qualify or SHUD_RHS_PACKED=0)");
     if (h->n_classes > 128) return shud_fail(SHUD_ERR_UNSUPPORTED, "lakes: more than 128 parameter classes");
     std::vector<int> lake_of(NE, -1), ele_off(NL + 1, 0), bank_off(NL + 1, 0), rin_off(NL + 1, 0);
@@ -823,19 +851,16 @@ static int setup_partition(shud_rhs *h, const ShudPartition *part) {
     HIP_TRY(hipEventCreateWithFlags(&h->ev_pack, hipEventDisableTiming | kEvSync));
     HIP_TRY(hipEventCreateWithFlags(&h->ev_comm, hipEventDisableTiming | kEvSync));
     if ((rc = h->upload(&h->d_halo_flag, (const unsigned long long *)nullptr, 1))) return rc;
-    const char *fe = getenv("SHUD_RHS_FOLD");
-    h->fold = !(fe && fe[0] == '0');
+    h->fold = env_knob("SHUD_RHS_FOLD", 1, 0, 1) != 0;
     // the trailing join of the comm stream after a folded eval costs ~4 us per eval at 8 ranks (one more packet for
     // the command processor between evals; profiles/r04/rankjoin): off by default.  Without it, after a poll timeout
     // (SHUD_EF_HALO_WAIT, fatal) the late pack / exchange may still run beside later main-stream work — results that
     // the fatal flag already invalidates; the error read (shud_read_err) drains the comm stream before reporting
-    const char *fj = getenv("SHUD_RHS_FOLD_JOIN");
-    h->fold_join = fj && fj[0] == '1';
+    h->fold_join = env_knob("SHUD_RHS_FOLD_JOIN", 0, 0, 1) != 0;
     int khz = 0;
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device) == hipSuccess && khz > 0)
         h->wall_khz = khz;
-    const char *tm = getenv("SHUD_HALO_TIMEOUT_MS");
-    const double ms = (tm && atof(tm) > 0) ? atof(tm) : 5000.0;
+    const double ms = env_knob("SHUD_HALO_TIMEOUT_MS", 5000, 1, 3600000);
     h->halo_timeout = (unsigned long long)(ms * h->wall_khz);
     return 0;
 }
@@ -985,7 +1010,7 @@ static void launch_ele(shud_rhs *h, const double *y, double *dy, int cur, int cu
     if (i1 < 0) i1 = h->n_own + h->n_segghost;
     // the last element launch of an eval (after the halo in every partitioned path) carries the QrivDown pre-pass
     const bool last = i1 == h->n_own + h->n_segghost;
-    if (h->packed && !h->variant) {
+    if (h->packed) {
         const bool qd = launch_element_kernel_packed(h->dm, h->dp, Y, dy, i0, i1, cur, h->mode, h->open, diag,
                                                      h->fu_unit[0] && h->fu_unit[1], h->dd, h->stream,
                                                      h->lakeon ? &h->lk : nullptr, h->partitioned && i1 <= h->n_int,
@@ -993,13 +1018,13 @@ static void launch_ele(shud_rhs *h, const double *y, double *dy, int cur, int cu
         if (last) h->qd_now = qd;
     } else {
         launch_element_kernel(h->dm, Y, dy, h->n_own + h->n_segghost, cur, cur_e, h->mode, h->open, diag, h->dd,
-                              h->stream, h->variant);
+                              h->stream);
         h->qd_now = false;
     }
 }
 static void launch_riv(shud_rhs *h, const double *y, double *dy, bool diag) {
     YView Y{y, h->d_gele, h->d_griv, h->n_own, h->n_own_riv};
-    if (h->packed && !h->variant)
+    if (h->packed)
         launch_river_kernel_packed(h->dm, h->dp, Y, dy, h->mode, diag, h->dd, h->stream, h->qd_now);
     else
         launch_river_kernel(h->dm, Y, dy, h->mode, diag, h->dd, h->stream);
@@ -1012,7 +1037,7 @@ static void launch_all(shud_rhs *h, const double *y, double *dy, int cur, int cu
 // carried-state ping-pong after an eval: the packed record carries {u_satn, e_ic} together
 static void flip(shud_rhs *h) {
     h->cur ^= 1;
-    if (h->packed && !h->variant) h->cur_e = h->cur;
+    if (h->packed) h->cur_e = h->cur;
     else if (h->mode == SHUD_MODE_SERIAL) h->cur_e ^= 1;
 }
 
@@ -1037,10 +1062,6 @@ static const uint32_t kFatal = SHUD_EF_NAN_QELE | SHUD_EF_EFFKH | SHUD_EF_ET_NEG
 
 // partitioned handles: the interior elements [0, n_int) run while the halo exchange is in flight (RCCL on
 // s_comm); boundary + ghost elements and the reaches wait for it.  Unpartitioned: one launch each.
-// SHUD_ABL_NOSPLIT (timing-only build, tools/rank_timing.py ablations): one element launch after the exchange
-#ifndef SHUD_ABL_NOSPLIT
-#define SHUD_ABL_NOSPLIT 0
-#endif
 // stream_halo: the halo is already ordered on the main stream (eval_compute, external transport) — the folded
 // launch's boundary workgroups then skip the flag
 static int launch_split(shud_rhs *h, const double *y, double *dy, hipEvent_t e_mid = nullptr,
@@ -1048,7 +1069,7 @@ static int launch_split(shud_rhs *h, const double *y, double *dy, hipEvent_t e_m
     // an RCCL communicator connects its peers lazily on the first send/recv (can take far longer than any eval):
     // that first exchange is waited for on the stream (split path), never polled by workgroups
     const bool first_rccl = h->use_nccl && h->n_exch <= 1 && !stream_halo;
-    if (h->fold && h->packed && !h->variant && !h->lakeon && !SHUD_ABL_NOSPLIT && !first_rccl) {
+    if (h->fold && h->packed && !h->lakeon && !first_rccl) {
         YView Y{y, h->d_gele, h->d_griv, h->n_own, h->n_own_riv};
         const HaloWait hw{h->d_halo_flag, stream_halo ? 0ull : h->halo_epoch, h->halo_timeout};
         if (launch_element_kernel_packed_fold(h->dm, h->dp, Y, dy, h->n_int, h->n_own + h->n_segghost, h->cur,
@@ -1064,7 +1085,7 @@ static int launch_split(shud_rhs *h, const double *y, double *dy, hipEvent_t e_m
             return 0;
         }
     }
-    if (h->partitioned && h->packed && !h->variant && h->n_int > 0 && !SHUD_ABL_NOSPLIT) {
+    if (h->partitioned && h->packed && h->n_int > 0) {
         launch_ele(h, y, dy, h->cur, h->cur_e, false, 0, h->n_int);
         HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_comm, 0));
         launch_ele(h, y, dy, h->cur, h->cur_e, false, h->n_int, h->n_own + h->n_segghost);
@@ -1072,6 +1093,19 @@ static int launch_split(shud_rhs *h, const double *y, double *dy, hipEvent_t e_m
         launch_riv(h, y, dy, false);
     } else {
         if (h->partitioned) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_comm, 0));
+        if (h->dp.rf_ntile > 0 && !h->partitioned) {          // river fold: one launch (build_river_fold)
+            YView Y{y, h->d_gele, h->d_griv, h->n_own, h->n_own_riv};
+            if (++h->rf_epoch == 0) h->rf_epoch = 1;
+            if (launch_rhs_packed_rf(h->dm, h->dp, Y, dy, h->n_own + h->n_segghost, h->cur, h->mode, h->open,
+                                     h->fu_unit[0] && h->fu_unit[1], h->dd, h->rf_epoch, h->rf_timeout, h->stream)) {
+                h->qd_now = true;
+                h->rf_now = true;
+                if (e_mid) HIP_TRY(hipEventRecord(e_mid, h->stream));
+                HIP_TRY(hipGetLastError());
+                return 0;
+            }
+        }
+        h->rf_now = false;
         launch_ele(h, y, dy, h->cur, h->cur_e, false);
         if (e_mid) HIP_TRY(hipEventRecord(e_mid, h->stream));
         launch_riv(h, y, dy, false);
@@ -1122,6 +1156,12 @@ extern "C" long long shud_rhs_num_calls(shud_rhs_t h) { return h ? h->ncalls : -
 extern "C" int shud_rhs_layout_streamed(shud_rhs_t h, int *n_streamed) {
     if (!h || !n_streamed) return shud_fail(SHUD_ERR_ARG, "null argument");
     *n_streamed = h->packed ? h->dp.nh : 0;
+    return SHUD_OK;
+}
+
+extern "C" int shud_rhs_layout_river_fold(shud_rhs_t h, int *folded) {
+    if (!h || !folded) return shud_fail(SHUD_ERR_ARG, "null argument");
+    *folded = h->dp.rf_ntile > 0 ? 1 : 0;
     return SHUD_OK;
 }
 
@@ -1189,8 +1229,7 @@ extern "C" int shud_rhs_cvrhs(double t, const double *y, double *ydot, void *use
     shud_rhs *h = (shud_rhs *)user_data;
     int rc = shud_rhs_eval(h, t, y, ydot, SHUD_WHERE_HOST);
     if (rc == SHUD_OK) return 0;
-    const char *strict = getenv("SHUD_RHS_STRICT_EXIT");
-    if (rc == SHUD_ERR_PHYSICS && strict && strict[0] == '1') {
+    if (rc == SHUD_ERR_PHYSICS && env_knob("SHUD_RHS_STRICT_EXIT", 0, 0, 1)) {
         ShudErr e;
         shud_rhs_get_error(h, &e);
         printf("\n%s\n", e.message);
@@ -1265,8 +1304,8 @@ extern "C" int shud_rhs_sync_diagnostics(shud_rhs_t h, ShudFluxOut *o) {
     std::vector<double> tmp;
     if (o->qseg_surf || o->qseg_sub) tmp.resize(std::max<size_t>(NS, 1));
     HIP_TRY(hipStreamSynchronize(h->stream));
-    const std::vector<int> &perm = (h->packed && h->dp.seg_rpos) ? h->rseg_perm : h->seg_perm;
-    if (h->packed && !h->variant && NS && (o->qseg_surf || o->qseg_sub)) {
+    const std::vector<int> &perm = h->seg_perm;
+    if (h->packed && NS && (o->qseg_surf || o->qseg_sub)) {
         std::vector<double2> q2(NS);
         HIP_TRY(hipMemcpy(q2.data(), h->dp.qseg2, NS * sizeof(double2), hipMemcpyDeviceToHost));
         for (size_t k = 0; k < NS; k++) {
@@ -1333,9 +1372,29 @@ extern "C" int shud_rhs_debug_halo(shud_rhs_t h, double spin_us, const double *d
     h->dbg_griv = d_riv_src;
     h->dbg_publish = publish != 0;
     h->dbg_armed = h->dbg_spin || d_ele_src || d_riv_src || !h->dbg_publish;
-    const char *tm = getenv("SHUD_HALO_TIMEOUT_MS");
-    const double ms = timeout_ms > 0 ? timeout_ms : (tm && atof(tm) > 0) ? atof(tm) : 5000.0;
+    const double ms = timeout_ms > 0 ? timeout_ms : env_knob("SHUD_HALO_TIMEOUT_MS", 5000, 1, 3600000);
     h->halo_timeout = (unsigned long long)(ms * h->wall_khz);
+    return SHUD_OK;
+}
+extern "C" int shud_rhs_debug_rfold(shud_rhs_t h, int tile, double spin_us, double timeout_ms, int *tile_out) {
+    if (!h || h->dp.rf_ntile <= 0) return shud_fail(SHUD_ERR_ARG, "not a river-folded handle");
+    if (spin_us < 0 || spin_us > 1e7) return shud_fail(SHUD_ERR_ARG, "spin_us out of range");
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    const EleGrid g = ele_grid(h->n_own + h->n_segghost, h->dp.nqd, h->dp.rf_qd_pm);
+    if (tile < 0) {                                   // the element tile the most reach tiles wait for
+        std::vector<int4> dep(h->dp.rf_ntile);
+        HIP_TRY(hipMemcpy(dep.data(), h->dp.rf_dep, dep.size() * sizeof(int4), hipMemcpyDeviceToHost));
+        std::vector<int> cnt(g.nb_e, 0);
+        for (const int4 &d : dep)
+            for (int t = d.x; t <= d.y; t++) cnt[t]++;
+        tile = (int)(std::max_element(cnt.begin(), cnt.end()) - cnt.begin());
+    }
+    if (tile >= g.nb_e) return shud_fail(SHUD_ERR_ARG, "tile %d out of range (%d element tiles)", tile, g.nb_e);
+    h->dp.rf_dbg_tile = tile;
+    h->dp.rf_dbg_ticks = (unsigned long long)(spin_us * 1e-3 * h->wall_khz);
+    if (timeout_ms > 0) h->rf_timeout = (unsigned long long)(timeout_ms * h->wall_khz);
+    if (tile_out) *tile_out = tile;
     return SHUD_OK;
 }
 // split eval for external transport: pack, (caller exchanges), compute

@@ -9,6 +9,9 @@
 //   3  one-shot read-only sweep (16-B non-temporal loads, 512-lane workgroups, a per-lane xor kept live by one
 //      conditional store): the read-side ceiling, which is what a read-dominated kernel such as the element
 //      kernel meets
+// and a pure fp64-VALU probe (shud_valu_probe): what the box's vector ALUs sustain and the clock they hold under a
+// dense fp64 load, so a bench line can say what kind of box it ran on (the element kernel's VALU issue floor is
+// ~0.67 of its cycles: its time follows the clock as well as the HBM rate).
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
@@ -89,4 +92,43 @@ extern "C" int shud_stream_copy_v(const void *src, void *dst, size_t bytes, void
 
 extern "C" int shud_stream_copy(const void *src, void *dst, size_t bytes, void *stream) {
     return shud_stream_copy_v(src, dst, bytes, stream, 0);
+}
+
+// fp64 VALU probe: 8 independent fma chains per lane (a[k] = a[k] * m + c, bounded: the fixed point is c / (1 - m)),
+// 2,048 workgroups of 256 lanes (8 waves per SIMD on 256 CUs), non-trivial operands (zero operands clock higher).
+// Lane 0 of every workgroup stamps s_memtime (shader clock) and s_memrealtime (100 MHz constant clock) around its
+// loop: the in-kernel clock is the ratio (MI355X_MICROARCH.md, DVFS give-back item 6).
+__global__ void __launch_bounds__(256) valu_probe_kernel(int iters, double m, double c, double *sink,
+                                                         unsigned long long *stamps) {
+    double a[8];
+    const double x0 = 0.5 + 1e-9 * (double)threadIdx.x + 1e-6 * (double)blockIdx.x;
+#pragma unroll
+    for (int k = 0; k < 8; k++) a[k] = x0 + 0.125 * k;
+    unsigned long long t0 = 0, r0 = 0;
+    if (threadIdx.x == 0) {
+        t0 = __builtin_amdgcn_s_memtime();
+        r0 = __builtin_amdgcn_s_memrealtime();
+    }
+    for (int i = 0; i < iters; i++) {
+#pragma unroll
+        for (int u = 0; u < 16; u++)
+#pragma unroll
+            for (int k = 0; k < 8; k++) a[k] = __builtin_fma(a[k], m, c);
+    }
+    if (threadIdx.x == 0) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        stamps[2 * blockIdx.x] = t1 - t0;
+        stamps[2 * blockIdx.x + 1] = r1 - r0;
+    }
+    double sum = 0.;
+#pragma unroll
+    for (int k = 0; k < 8; k++) sum += a[k];
+    if (sum == 12345.678) sink[threadIdx.x] = sum;                  // keeps the chains live; never taken
+}
+// fp64 FMAs per launch = blocks x 256 x iters x 128; stamps: [2 * blocks] (shader cycles, 100 MHz ticks) per block
+extern "C" int shud_valu_probe(int blocks, int iters, double *sink, unsigned long long *stamps, void *stream) {
+    if (blocks <= 0 || iters <= 0) return -2;
+    hipLaunchKernelGGL(valu_probe_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, iters, 0.9999999999, 1e-12,
+                       sink, stamps);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -325,10 +325,44 @@ def test_many_classes(oracle_mod, monkeypatch, kind):
                           label=f"many-class {kind}", layout="soa" if kind == "soa" else "packed")
 
 
+def _class_count(m):
+    """distinct parameter tuples of a model (the packed layout's classes: shud_rhs.cpp build_packed)"""
+    keys = ["macD", "macKsatH", "geo_vAreaF", "KsatH", "KsatV", "infKsatV", "hAreaF", "macKsatV", "ThetaS", "ThetaR",
+            "Beta", "infD", "Sy", "RzD", "VegFrac", "ImpAF"]
+    cols = [np.asarray(m.par[k], np.float64) for k in keys] + [np.asarray(m.ele["depression"], np.float64),
+                                                               np.asarray(m.ele["rough"], np.float64)]
+    return np.unique(np.stack(cols, 1), axis=0).shape[0]
+
+
+@pytest.mark.parametrize("target", ["mid", "max"])
+def test_lds_big_class_table(oracle_mod, monkeypatch, target):
+    """129..560 parameter classes with the hybrid layout off (SHUD_RHS_HYB=0): the 1024-thread workgroups that stage
+    the whole class table + pow tables in LDS (shud_ele_kernel_packed_big), serial and OMP, against the oracle.
+    "max" sits at the LDS bound (kLdsClassMaxBig = 560 classes: the dynamic-LDS attribute and the 16-B table copy at
+    their largest)."""
+    monkeypatch.setenv("SHUD_RHS_HYB", "0")
+    m, y = cases.variant(20000, seed=29)
+    base, k = m.par["KsatH"].copy(), np.arange(m.num_ele)
+    mult, n = 12, 0
+    for mm in ([12] if target == "mid" else range(12, 40)):    # "max": the most classes still <= 560
+        m.par["KsatH"] = base * (1.0 + 1e-7 * (k % mm))
+        nn = _class_count(m)
+        if nn > 560:
+            break
+        mult, n = mm, nn
+    m.par["KsatH"] = base * (1.0 + 1e-7 * (k % mult))
+    assert 128 < n <= 560 and (target == "mid" or n > 520), (mult, n)
+    lay = _runtime().RhsHandle(m).layout()
+    assert lay["packed"] and not lay.get("streamed_fields") and lay["n_classes"] == n, lay
+    for mode in (abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP):
+        _compare_sequence(m, [y] + cases.states(m, None, 1, seed=7), mode, oracle_mod, ncalls=2,
+                          label=f"big class table {n}", layout="packed")
+
+
 @pytest.mark.parametrize("mode", [abi.SHUD_MODE_SERIAL, abi.SHUD_MODE_OMP])
 def test_mid_class_count(mode, oracle_mod):
     """~66 parameter classes: the LDS class table without the DY-tail LDS slots (they fit beside tables of up to
-    ~35 classes only, shud_ele_packed.hip SHUD_LSPILL), against the oracle."""
+    ~35 classes only, shud_ele_packed.hip LSP), against the oracle."""
     m, y = cases.variant(20000, seed=23)
     m.par["KsatH"] = m.par["KsatH"] * (1.0 + 1e-7 * (np.arange(m.num_ele) % 2))
     lay = _runtime().RhsHandle(m, mode=mode).layout()

@@ -169,30 +169,6 @@ def test_device_leaf_kat_vs_oracle(name):
 
 
 @pytest.mark.gpu
-def test_pow_pos_bit_identical():
-    """pow_pos (shud_physics.h: OCML's pow core without its special-case selects) returns the same bits as the
-    device's full pow on satKfun's domain — bases in (0, 1] (satn in (ZERO, 0.99], 1 - satn^ex1), exponents
-    n/(n-1) and (n-1)/n of Beta > 1 — and on a wider positive grid."""
-    lib = C.CDLL(os.path.join(PKG_DIR, "libshud_kat.so"))
-    lib.shud_kat_pow.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_void_p]
-    rng = np.random.default_rng(7)
-    n = 1 << 20
-    beta = np.concatenate([1.0 + rng.uniform(1e-6, 4.0, n // 2), 1.0 + 10 ** rng.uniform(-12, 3, n // 2)])
-    x = np.concatenate([rng.uniform(1e-10, 0.99, n // 4), 10 ** rng.uniform(-10, 0, n // 4),
-                        1.0 - 10 ** rng.uniform(-17, -0.01, n // 4), 10 ** rng.uniform(-300, 300, n // 4)])
-    y = np.where(rng.random(n) < 0.5, beta / (beta - 1.0), (beta - 1.0) / beta)
-    edge_x = np.array([1.0, 0.99, 1e-10, 0.5, np.nextafter(1.0, 0.0), 5e-324, 2.2250738585072014e-308])
-    edge_y = np.array([3.0, 1.0, 0.5, 2.0, 1e6, 1.0, 1.0])
-    xy = np.ascontiguousarray(np.stack([np.concatenate([x, edge_x]), np.concatenate([y, edge_y])], 1))
-    m = xy.shape[0]
-    full, fast = np.zeros(m), np.zeros(m)
-    assert lib.shud_kat_pow(0, xy.ctypes.data, m, full.ctypes.data) == 0
-    assert lib.shud_kat_pow(1, xy.ctypes.data, m, fast.ctypes.data) == 0
-    same = full.view(np.uint64) == fast.view(np.uint64)
-    assert same.all(), f"{(~same).sum()} differ, first (x, y) = {xy[np.argmax(~same)]}"
-
-
-@pytest.mark.gpu
 def test_cos_small_bit_identical():
     """cos_small (shud_physics.h: OCML's small-argument cos path without the Payne-Hanek branch and the |x| /
     finiteness selects) returns the same bits as the device's full cos on SoilMoistureStress's arguments
@@ -277,6 +253,70 @@ def test_cdiv_bit_identical():
     assert lib.shud_kat_cdiv(a.ctypes.data, b.ctypes.data, a.size, got.ctypes.data) == 0
     ok = _bits_same(got, want)
     assert ok.all(), f"{(~ok).sum()} differ, first (a, b) = {a[np.argmax(~ok)]!r}, {b[np.argmax(~ok)]!r}"
+
+
+def _fast_operands(n=1 << 21, seed=23):
+    """the fast paths' domains and edges: random bit patterns (every class and exponent), magnitudes 10^-320..10^308,
+    Manning slopes and weir depths, values straddling the guard bounds 2^-767 (sqrt), 2^-900 / 2^600 (numerator),
+    2^-100 / 2^100 (divisor), signed zeros, infinities, NaN"""
+    rng = np.random.default_rng(seed)
+    raw = rng.integers(0, 2 ** 63, n // 4, dtype=np.uint64).view(np.float64) * rng.choice([-1.0, 1.0], n // 4)
+    mag = 10 ** rng.uniform(-320, 308, n // 4) * rng.choice([-1.0, 1.0], n // 4)
+    phys = rng.uniform(-2.0, 2.0, n // 4) * 10 ** rng.uniform(-12, 3, n // 4)
+    edges = []
+    for e in (-767, -900, 600, -100, 100, -1022, 1023, 0):
+        edges.append(np.ldexp(1.0, e) * np.array([1.0, 1.0 - 2 ** -53, 1.0 + 2 ** -52, -1.0]))
+    edges.append(np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 5e-324, -5e-324, 2.2250738585072014e-308,
+                           1.7976931348623157e308]))
+    rest = 10 ** rng.uniform(-5, 5, n // 4)
+    a = np.concatenate([raw, mag, phys, rest] + edges)
+    b = np.concatenate([rng.permutation(a[: a.size - sum(e.size for e in edges)])] +
+                       [10 ** rng.uniform(-40, 40, sum(e.size for e in edges))])
+    b = np.where(rng.random(b.size) < 0.5, b, np.ldexp(rng.uniform(0.5, 1.0, b.size),
+                                                        rng.integers(-110, 110, b.size)) * rng.choice([-1.0, 1.0], b.size))
+    return a, b
+
+
+@pytest.mark.gpu
+def test_fast_sqrt_div_bit_identical():
+    """shud_physics.h sqrt_nr (LLVM's f64 sqrt chain without its tiny-argument scaling and zero/inf select, those on a
+    cold path) and div_nr / recip_nr (the f64 division chain without v_div_scale / v_div_fixup, the reciprocal shared
+    by divisions with one divisor) return the same bits as the device's own sqrt and a / b on every operand class."""
+    lib = C.CDLL(os.path.join(PKG_DIR, "libshud_kat.so"))
+    lib.shud_kat_fast.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+    a, b = _fast_operands()
+    a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+    out = [np.zeros_like(a) for _ in range(4)]
+    for k in range(4):
+        assert lib.shud_kat_fast(k, a.ctypes.data, b.ctypes.data, a.size, out[k].ctypes.data) == 0
+    for fast, ref, name in ((0, 1, "sqrt_nr"), (2, 3, "div_nr")):
+        ok = _bits_same(out[fast], out[ref])
+        assert ok.all(), f"{name}: {(~ok).sum()} differ, first (a, b) = {a[np.argmax(~ok)]!r}, {b[np.argmax(~ok)]!r}"
+    with np.errstate(all="ignore"):                 # and both are the IEEE results (correctly rounded)
+        assert _bits_same(out[1], np.sqrt(a)).all()
+        assert _bits_same(out[3], a / b).all()
+
+
+@pytest.mark.gpu
+def test_cbrt_glibc_bit_identical():
+    """shud_physics.h cbrt_glibc (glibc 2.35's s_cbrt.c restated for the device; pow23 / Manning's R^(2/3),
+    Equations.hpp:36-39) equals this host's glibc cbrt (libm.so.6 via ctypes) bit for bit: Manning's domain (hydraulic radius and
+    surface depth 1e-12 .. 1e3), every exponent (incl. subnormals), signed zeros, infinities and NaN."""
+    lib = C.CDLL(os.path.join(PKG_DIR, "libshud_kat.so"))
+    lib.shud_kat_fast.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+    rng = np.random.default_rng(29)
+    n = 1 << 19
+    a = np.concatenate([10 ** rng.uniform(-12, 3, n // 2), rng.uniform(0.0, 0.5, n // 4),
+                        10 ** rng.uniform(-323, 308, n // 4) * rng.choice([-1.0, 1.0], n // 4),
+                        np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 5e-324, 1.0, 8.0, -27.0, 0.5, 2.0 ** -1074])])
+    a = np.ascontiguousarray(a)
+    got = np.zeros_like(a)
+    assert lib.shud_kat_fast(4, a.ctypes.data, a.ctypes.data, a.size, got.ctypes.data) == 0
+    libm = C.CDLL("libm.so.6")                    # glibc's own cbrt (numpy.cbrt is numpy's implementation, not libm's)
+    libm.cbrt.restype, libm.cbrt.argtypes = C.c_double, [C.c_double]
+    want = np.array([libm.cbrt(float(x)) for x in a])
+    ok = _bits_same(got, want)
+    assert ok.all(), f"{(~ok).sum()} differ, first x = {a[np.argmax(~ok)]!r}"
 
 
 # ---- pow_tab (shud_powtab.h): satKfun's pow ----------------------------------------------------------------------

@@ -19,9 +19,9 @@ from shud_rhs import abi, runtime, synth, workload  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--n-ele", type=int, default=10_000_000)
-ap.add_argument("--variants", default="soa0,soa3,pk,pk4,pk5",
-                help="soaK = SoA kernel build variant K (SHUD_RHS_PACKED=0, SHUD_RHS_ELE_VARIANT=K); "
-                     "pk / pkW = packed class-layout kernel (min W waves/SIMD)")
+ap.add_argument("--variants", default="soa,pk",
+                help="soa = the SoA kernel (SHUD_RHS_PACKED=0); pk = the packed class-layout kernel; "
+                     "pk+NAME=VAL = pk with run-time switches; lib:NAME = an A/B library build")
 ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--many-class", action="store_true",
@@ -51,17 +51,16 @@ def lib_for(v):
 def env_for(v):
     # pk+NAME=VAL[+NAME=VAL]: the packed kernel with extra environment (run-time switches, e.g. pk+SHUD_RHS_QD=0)
     if v.startswith("pk+"):
-        e = {"SHUD_RHS_PACKED": "1", "SHUD_RHS_ELE_VARIANT": "0", "SHUD_RHS_SEG_ORDER": "element"}
+        e = {"SHUD_RHS_PACKED": "1"}
         e.update(kv.split("=", 1) for kv in v[3:].split("+"))
         return e
     if v.startswith("lib:"):     # lib:NAME[+NAME=VAL...]: an A/B library, optionally with run-time switches
-        e = {"SHUD_RHS_PACKED": "1", "SHUD_RHS_ELE_VARIANT": "0", "SHUD_RHS_SEG_ORDER": "element"}
+        e = {"SHUD_RHS_PACKED": "1"}
         e.update(kv.split("=", 1) for kv in v[4:].split("+")[1:])
         return e
     if v.startswith("soa"):
-        return {"SHUD_RHS_PACKED": "0", "SHUD_RHS_ELE_VARIANT": v[3:] or "0"}
-    return {"SHUD_RHS_PACKED": "1", "SHUD_RHS_ELE_VARIANT": "0",
-            "SHUD_RHS_SEG_ORDER": "reach" if v == "pkR" else "element"}
+        return {"SHUD_RHS_PACKED": "0"}
+    return {"SHUD_RHS_PACKED": "1"}
 res = {v: [] for v in vs}
 rres = {v: [] for v in vs}
 wres = {v: [] for v in vs}

@@ -56,9 +56,9 @@ for step in "$@"; do
       tail -n 1 "$O/abl.log" > "$O/abl_summary.log" ;;
     ab:*)
       libs="${step#ab:}"
-      timeout -k 10 300 python tools/ab_variants.py --variants soa0,pk --rounds 5 > "$O/ab_prod.log" 2>&1
+      timeout -k 10 300 python tools/ab_variants.py --variants soa,pk --rounds 5 > "$O/ab_prod.log" 2>&1
       for n in ${libs//,/ }; do
-        SHUD_RHS_LIB=$PWD/shud-up_amd/build/ab/libshud_rhs_$n.so timeout -k 10 300 python tools/ab_variants.py --variants soa0,pk --rounds 5 > "$O/ab_$n.log" 2>&1
+        SHUD_RHS_LIB=$PWD/shud-up_amd/build/ab/libshud_rhs_$n.so timeout -k 10 300 python tools/ab_variants.py --variants soa,pk --rounds 5 > "$O/ab_$n.log" 2>&1
       done
       for f in prod ${libs//,/ }; do echo "$f $(tail -n 1 "$O/ab_$f.log")"; done > "$O/ab_summary.log" ;;
     odeab:*)
@@ -110,10 +110,6 @@ for step in "$@"; do
     e2e) timeout -k 10 600 bash tools/profile_e2e.sh 1000000 1 > "$O/e2e.log" 2>&1 ;;
     traj) timeout -k 10 300 python tests/diag_traj_day.py "$O/traj_ccw_day.json" > "$O/traj_ccw_day.log" 2>&1 ;;
     classes) timeout -k 10 600 python tools/class_sweep.py > "$O/class_sweep.log" 2>&1 ;;
-    rivorder) timeout -k 10 600 python -u tools/riv_order_ab.py > "$O/riv_order.log" 2>&1 ;;   # caller reach numberings band / dfs / bfs
-    rivorder:*)                 # rivorder:L1,L2 -> the same with A/B libs (e.g. SHUD_RIV_ABL builds) timed beside production
-      libs=""; for l in $(echo "${step#rivorder:}" | tr , ' '); do libs="$libs --lib $l"; done
-      timeout -k 10 900 python -u tools/riv_order_ab.py --orders band,dfs $libs > "$O/riv_order_libs.log" 2>&1 ;;
     redbench) timeout -k 10 120 tools/ode_red_bench 31000000 30 > "$O/ode_red_bench.log" 2>&1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
