@@ -375,11 +375,7 @@ def main():
 
     # per-kernel times: HIP events recorded inside the timed loop on the handle's stream (= torch's current
     # stream); a partitioned handle also gets a serialized per-phase breakdown (halo exchange alone)
-    # river fold: the reaches ride in the element launch, so the "element kernel" events bracket the
-    # one launch that does both (shud_rhs_kernel_packed_rf) and the river slot reads ~0
-    folded = bool(h.layout().get("river_fold"))
-    per = ({"shud_rhs_kernel_rf": ms_ele_loop} if folded else
-           {"shud_ele_kernel": ms_ele_loop, "shud_riv_kernel": ms_riv_loop})
+    per = {"shud_ele_kernel": ms_ele_loop, "shud_riv_kernel": ms_riv_loop}
     ms_eval = ms_eval_loop
     if world > 1 and args.profile_reps > 0:
         _, per_ser = h.time_kernels(0.0, yp, dyp, args.profile_reps)
@@ -388,15 +384,14 @@ def main():
         dist.all_reduce(th, op=dist.ReduceOp.MAX)
         per["halo_exchange_serialized"] = float(th.item())
         dist.barrier()
-    ms_ele = per["shud_rhs_kernel_rf"] if folded else per["shud_ele_kernel"]
-    ms_riv = 0.0 if folded else per["shud_riv_kernel"]
+    ms_ele = per["shud_ele_kernel"]
+    ms_riv = per["shud_riv_kernel"]
     n_own_e = model.num_ele if world == 1 else part.n_own_ele
     n_own_r = model.num_riv if world == 1 else part.n_own_riv
     n_seg_local = model.num_seg
     ele_bytes = B_ELE * n_own_e + B_SEG * n_seg_local
     riv_bytes = B_RIV * n_own_r
-    dom_bytes = ele_bytes + riv_bytes if folded else ele_bytes      # the dominant launch's algorithmic bytes
-    achieved = dom_bytes / (ms_ele * 1e-3)
+    achieved = ele_bytes / (ms_ele * 1e-3)
 
     value = NE * args.steps / dt
     ms_step = dt / args.steps * 1e3
@@ -424,14 +419,13 @@ def main():
                    "y_ydot": "device-resident", "kernel_layout": h.layout()},
         "roofline": {
             "bound": "hbm",
-            "kernel": ("shud_rhs_kernel_rf (elements + QrivDown pre-pass + reaches, one launch)" if folded
-                       else "shud_ele_kernel"),
+            "kernel": "shud_ele_kernel",
             "achieved": achieved / 1e9,
             "peak": HBM_PEAK / 1e9,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK,
             "traffic": None,
-            "algorithmic_bytes_per_launch": dom_bytes,
+            "algorithmic_bytes_per_launch": ele_bytes,
             "kernel_ms": {k: v for k, v in per.items()},
             "kernel_ms_source": (f"HIP events around the kernels of {n_timed} of the {args.steps} timed evals "
                                  f"(1 in {t_stride}; handle stream)"),
@@ -469,7 +463,7 @@ def main():
                                                             f"{FP64_VALU_NOMINAL / 1e12:g} TFLOP/s)")
         out["box"] = box
     if world == 1:
-        tr = pmc_traffic(NE, "shud_rhs_kernel_rf" if folded else "shud_ele_kernel")
+        tr = pmc_traffic(NE)
         out["roofline"].update(tr)
         if out["roofline"].get("traffic"):
             out["roofline"]["frac_actual"] = out["roofline"]["traffic"] / (ms_ele * 1e-3) / HBM_PEAK

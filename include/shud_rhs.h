@@ -189,10 +189,6 @@ int  shud_rhs_layout(shud_rhs_t h, int *packed, int *n_classes);
  * depression, Rough) are streamed per element because the full parameter tuples exceed one workgroup's LDS class
  * table (per-element-calibrated models); 0 = every field from the class table */
 int  shud_rhs_layout_streamed(shud_rhs_t h, int *n_streamed);
-/* *folded = 1 when an ordinary eval runs the elements, the QrivDown pre-pass and the reaches in ONE launch (the reach
- * tiles start once the element tiles they read have published: unpartitioned, lake-free handles on the LDS class
- * table); 0 = an element launch, then a river launch.  Same results either way. */
-int  shud_rhs_layout_river_fold(shud_rhs_t h, int *folded);
 int  shud_rhs_destroy(shud_rhs_t h);
 const char *shud_rhs_last_error_string(void);
 
@@ -259,13 +255,6 @@ int  shud_rhs_eval_compute(shud_rhs_t h, double t, const double *d_y, double *d_
  * SHUD_HALO_TIMEOUT_MS or 5000).  spin_us 0, NULL sources and publish 1 disarm the hook. */
 int  shud_rhs_debug_halo(shud_rhs_t h, double spin_us, const double *d_ele_src, const double *d_riv_src,
                          int publish, double timeout_ms);
-
-/* Test hook (no reference analogue; tests/test_gpu_parity.py): in every following folded eval
- * (shud_rhs_layout_river_fold) the workgroup of element tile `tile` (256 elements; tile < 0: the one the most reach
- * tiles wait for) spins spin_us microseconds before its elements, so the reach tiles that read its segment fluxes
- * must wait for its flag; timeout_ms > 0 sets their poll bound (a spin past it: SHUD_EF_HALO_WAIT).  *tile_out: the
- * tile armed.  spin_us 0 disarms. */
-int  shud_rhs_debug_rfold(shud_rhs_t h, int tile, double spin_us, double timeout_ms, int *tile_out);
 
 int  shud_rhs_nccl_unique_id(char out[128]);
 int  shud_rhs_create_partitioned(const ShudMeshSoA *mesh, const ShudParamsSoA *par,

@@ -151,35 +151,7 @@ struct DevPacked {
     int qd_pm, qd_pm_fold;  // where the QrivDown blocks sit in the element launch: after this many permille of its
                             //   element blocks (single launch / folded partition launch; SHUD_QD_POS[_FOLD])
     int lds_big;            // 1: 129..kLdsClassMaxBig classes take the 1024-thread LDS-table kernel (host dispatch)
-    // river fold (unpartitioned, lake-free handles on the LDS class table): the reach tiles ride in the last blocks of
-    // the element launch and start once the element tiles and QrivDown blocks whose results they read have published
-    // them (shud_ele_packed.hip shud_rhs_kernel_packed_rf)
-    unsigned *rf_flag;      // [nb_e + nb_q] the eval's epoch once an element tile / QrivDown block's stores are out
-    const int *rf_tile;     // [rf_ntile] river block -> reach tile, in the order their inputs come due
-    const int4 *rf_dep;     // [rf_ntile] per reach tile {first, last element tile, first, last QrivDown block} it reads
-    int rf_ntile;           // reach tiles (256 reaches each); 0: no fold
-    int rf_qd_pm;           // where the QrivDown blocks sit in the folded launch (permille of the element blocks)
-    int rf_dbg_tile;        // test hook (shud_rhs_debug_rfold): this element tile spins rf_dbg_ticks before its work
-    unsigned long long rf_dbg_ticks;
 };
-// block geometry of the element launch (shared by the launcher and the host's river-fold dependency tables): nb_e element
-// blocks (256 elements each, padded to a multiple of 8 so the XCD chunks are whole), nb_q QrivDown blocks placed after
-// the first q0 element blocks
-struct EleGrid {
-    int nb_e, nb_q, q0;
-    int per8() const { return nb_e / 8; }
-    // launch block of element tile t (tile_of's inverse) and of QrivDown block qb
-    int block_of_tile(int t) const { const int eb = (t % per8()) * 8 + t / per8(); return eb < q0 ? eb : eb + nb_q; }
-    int block_of_qd(int qb) const { return q0 + qb; }
-};
-inline EleGrid ele_grid(int n, int nqd, int pm) {
-    EleGrid g;
-    g.nb_e = ((n + 255) / 256 + 7) / 8 * 8;
-    g.nb_q = nqd > 0 ? ((nqd + 255) / 256 + 7) / 8 * 8 : 0;
-    const int pc = pm < 0 ? 0 : pm > 1000 ? 1000 : pm;
-    g.q0 = (int)((long long)g.nb_e * pc / 1000 / 8 * 8);
-    return g;
-}
 
 struct DevDiag {                     // optional diagnostic outputs (ShudFluxOut), local numbering
     double *qele_surf, *qele_sub, *qele_surf_tot, *qele_sub_tot, *q_infil, *q_exfil, *q_recharge;
@@ -242,12 +214,6 @@ bool launch_element_kernel_packed_fold(const DevMesh &m, const DevPacked &p, con
                                        int n_all, int cur, int mode, bool open, bool fu_unit, const DevDiag &dg,
                                        const HaloWait &hw, hipStream_t s, bool with_qd = false);
 void launch_halo_flag(unsigned long long *flag, unsigned long long epoch, hipStream_t s);
-// river fold: the elements [0, n), the QrivDown pre-pass and the reaches in ONE launch (DevPacked::rf_*); epoch: this
-// eval's flag value (never 0); timeout: wall-clock ticks a reach tile polls before SHUD_EF_HALO_WAIT.  false: this
-// configuration has no folded instantiation (the caller launches the element and river kernels)
-bool launch_rhs_packed_rf(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int n, int cur, int mode,
-                          bool open, bool fu_unit, const DevDiag &dg, unsigned epoch, unsigned long long timeout,
-                          hipStream_t s);
 // test hooks (shud_rhs_debug_halo): a one-lane spin of `ticks` wall-clock ticks, and a plain vector copy (the
 // stand-in for RCCL's receive kernels writing the ghost buffers), both on the comm stream
 void launch_spin(unsigned long long ticks, hipStream_t s);

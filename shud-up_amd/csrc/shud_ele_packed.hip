@@ -42,18 +42,6 @@ __device__ __forceinline__ void stnt2(double2 *p, double a, double b) {
     v.y = b;
     __builtin_nontemporal_store(v, (v2d *)p);
 }
-// one 16-byte write-through store (buffer_store_dwordx4 ... sc1): the line goes to memory at once and leaves this XCD's
-// L2, so a workgroup of the same launch on another XCD that reads it after the producer's flag sees the new bytes
-// (MI355X guide Guideline 16 R1: write-through payload, drained, then one flag store; no release fence).  off: bytes
-// from base, below 2 GiB (qseg2: 16 B x NS, NS < 2^27 by the handle's 32-bit stream offsets)
-__device__ __forceinline__ void st_wt16(double2 *base, uint32_t off, double a, double b) {
-    typedef unsigned v4u __attribute__((ext_vector_type(4)));
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
-    const unsigned long long ua = __builtin_bit_cast(unsigned long long, a), ub = __builtin_bit_cast(unsigned long long, b);
-    v4u v;
-    v.x = (unsigned)ua; v.y = (unsigned)(ua >> 32); v.z = (unsigned)ub; v.w = (unsigned)(ub >> 32);
-    __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)off, 0, 16);     // aux 16 = sc1
-}
 // element / segment streams are addressed as a wave-uniform base + a 32-bit byte offset, which the compiler
 // emits as global_load/store v, vOff, s[base] (saddr form): one 32-bit shift per record size shared by every
 // stream of that size, instead of a sign extension and a 64-bit address add per stream.  The handle keeps
@@ -182,7 +170,7 @@ __device__ __forceinline__ int tile_of(int per8) { return tile_of(per8, (int)blo
 // kernel reads them, early enough that their dependent loads overlap element work instead of forming the launch's
 // tail.  q0 and nb_q are multiples of 8, so the element tiles keep their XCD chunks.
 struct HaloWait;
-template <int MODE, bool HALO, bool WT = false>
+template <int MODE, bool HALO>
 __device__ __forceinline__ void qd_pre(const DevMesh &m, const DevPacked &p, const YView &Y, int r, int n_int,
                                        const HaloWait *hw);
 // block b -> QrivDown block (>= 0, *e untouched) or -1 with *e = the element block ordinal
@@ -192,8 +180,7 @@ __device__ __forceinline__ int qd_split(int b, int nb_q, int q0, int *e) {
     return -1;
 }
 
-template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB = 0, int LSP = 0,
-          bool WT = false>
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB = 0, int LSP = 0>
 __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, const YView &Y, double *__restrict__ dy,
                                          int i, int cur, const DevDiag &dg, const DevLake &lk, const double *lct,
                                          const OwnRec &own);
@@ -360,7 +347,7 @@ __device__ __forceinline__ void hload(const DevPacked &p, int i, double (&v)[4])
 // (Edge j+1's neighbour gathers issued at the top of edge j's iteration, or edge 0's before the segment loop: 92 / 94
 // VGPRs, 5 waves per SIMD, element kernel 0.620 / 0.627 vs 0.600 ms; forced to 6 waves it spills (0.752).  Occupancy
 // hides the gathers' latency better than the extra loads in flight per wave, profiles/r05/edge_pf/.)
-template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB, int LSP, bool WT>
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB, int LSP>
 __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, const YView &Y, double *__restrict__ dy,
                                          int i, int cur, const DevDiag &dg, const DevLake &lk, const double *lct,
                                          const OwnRec &own) {
@@ -537,8 +524,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
             const double rdep = dk.x, L = lc.x;
             const double qs = weir_jtoi(zs, isf_seg, zs - rdep, yr, zs + 0.0, lc.y, L, dep);
             const double qg = r2e_gw(yr, zs - rdep, ugw, zb, ekh, dk.y, L, bt) * fu_sub;
-            if (WT) st_wt16(p.qseg2, k16, qs, qg);                       // element-sorted; river fold: write-through
-            else *atw(p.qseg2, k16) = make_double2(qs, qg);
+            *atw(p.qseg2, k16) = make_double2(qs, qg);                  // element-sorted
             qe2r_surf += -qs;
             qe2r_sub += -qg;
         }
@@ -731,7 +717,7 @@ __device__ __forceinline__ double riv_down_outlet(const RivP &q, double uq, cons
 // HALO (the folded partition launch): a wave with a lane whose reach or downstream is a ghost takes the halo
 // wait (poll + agent acquire, which invalidates the CU's L1) before its stage loads; the others — nearly all —
 // read only owned stages and skip it.  r < 0: an idle lane (still reaches the wave-wide ballot).
-template <int MODE, bool HALO, bool WT>
+template <int MODE, bool HALO>
 __device__ __forceinline__ void qd_pre(const DevMesh &m, const DevPacked &p, const YView &Y, int r, int n_int,
                                        const HaloWait *hw) {
     const int rr = r < 0 ? 0 : r;
@@ -748,10 +734,7 @@ __device__ __forceinline__ void qd_pre(const DevMesh &m, const DevPacked &p, con
     const double2 bd = p.rv[4 * (size_t)d + 1], dd = p.rv[4 * (size_t)d + 3];
     double ydg;
     const double ud = riv_stage_p<MODE>(m, Y, d, rv_ib(dd.y).y, &ydg);
-    const double qd = riv_down_p(q, ur, g, ud, dd.x, bd.y);
-    if (WT) __hip_atomic_store((unsigned long long *)p.qdown + r, __builtin_bit_cast(unsigned long long, qd),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // write-through (sc1): river fold
-    else p.qdown[r] = qd;
+    p.qdown[r] = riv_down_p(q, ur, g, ud, dd.x, bd.y);
 }
 
 // dword-aligned 16-B / 8-B loads of index words (gfx950 global loads need only 4-B alignment for dwordx4)
@@ -854,107 +837,6 @@ shud_riv_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy,
     const int r = tile_of(per8) * 256 + (int)threadIdx.x;
     if (r >= Y.n_own_riv) return;
     riv_body<MODE, DIAG, SB, QD>(m, p, Y, dy, dg, r);
-}
-
-// ===================================================================================
-// River fold: elements, QrivDown pre-pass and reaches in ONE launch (unpartitioned, lake-free, LDS class table).
-// Blocks [0, nb_e + nb_q) are the element tiles and the QrivDown blocks of the single launch; the reach tiles follow in
-// blocks nb_e + nb_q .. (DevPacked::rf_tile: in the order their inputs come due), so a reach tile whose elements are
-// done runs in the slots the element launch's tail leaves idle instead of after it (the river kernel was 7 % of every
-// RHS, latency-bound on dependent gathers).  Hand-off (MI355X guide Guideline 16 R1): every element tile and QrivDown
-// block stores its qseg2 / qdown results write-through (sc1), drains them (vmcnt(0) in every wave), meets a workgroup
-// barrier, and one lane stores the eval's epoch into its flag (agent scope); a reach tile's wave 0 polls the flags of
-// the element tiles owning every 128-B qseg2 line it reads and of the QrivDown blocks of its own and upstream reaches
-// (DevPacked::rf_dep, host-computed), then ONE agent acquire, a workgroup barrier, plain loads.  Reach tiles sit after
-// every element and QrivDown block, so once dispatched, all they wait for is resident or done; the poll is bounded all
-// the same (wall clock, then the fatal SHUD_EF_HALO_WAIT).  Same arithmetic as the two launches: bit-identical.
-// ===================================================================================
-#ifndef SHUD_RF_DIAG
-#define SHUD_RF_DIAG 0      // TEMP timing-only: 1 no poll, 2 no publish + no poll, 4 plain stores
-#endif
-__device__ __forceinline__ void rf_publish(unsigned *flag, unsigned epoch) {
-    if (SHUD_RF_DIAG & 2) return;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // every wave: its write-through stores are out
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// each wave drains its own stores and counts itself in an LDS word; the wave that completes the count publishes (MI355X
-// guide Valid forms, Producer: "each wave adds to a counter in LDS after its wait and the wave whose add is last
-// signals") — no workgroup barrier at the end, so early waves leave as soon as their own stores are out
-__device__ __forceinline__ void rf_publish_lds(unsigned *flag, unsigned epoch, unsigned *cnt) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    unsigned old = 0;
-    if (__lane_id() == 0) old = atomicAdd(cnt, 1u);
-    old = __shfl(old, 0);
-    if (old == (kEleBS / 64) - 1 && __lane_id() == 0)
-        __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <int MODE>
-__device__ __forceinline__ void rf_reach_tile(const DevMesh &m, const DevPacked &p, const YView &Y, double *__restrict__ dy,
-                                              const DevDiag &dg, int tile, int nb_e, unsigned epoch,
-                                              unsigned long long timeout) {
-    if (!(SHUD_RF_DIAG & 3) && threadIdx.x < 64) {            // wave 0 polls every flag this tile's inputs carry
-        const int4 d = p.rf_dep[tile];
-        const int ne = d.y - d.x + 1, n = ne + (d.w - d.z + 1);
-        const int lane = (int)threadIdx.x;
-        const unsigned long long t0 = wall_clock64();
-        bool late = false;
-        for (;;) {
-            bool ok = true;
-            for (int k = lane; k < n; k += 64) {
-                const int f = k < ne ? d.x + k : nb_e + d.z + (k - ne);
-                ok &= __hip_atomic_load(p.rf_flag + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
-            }
-            if (__builtin_amdgcn_ballot_w64(!ok) == 0ull) break;
-            if (wall_clock64() - t0 > timeout) { late = true; break; }
-            __builtin_amdgcn_s_sleep(2);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        report_w(m.err, late, 0x80u, 7, tile * 256);           // SHUD_EF_HALO_WAIT (a timed-out wait)
-    }
-    __syncthreads();
-    const int r = tile * 256 + (int)threadIdx.x;
-    if (r < Y.n_own_riv) riv_body<MODE, false, 6, true>(m, p, Y, dy, dg, r);
-}
-template <int MODE, bool OPEN, bool FU1, int LSPK>
-__global__ void __launch_bounds__(kEleBS, kEleWaves)
-shud_rhs_kernel_packed_rf(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int n_compute, int cur, DevDiag dg,
-                          int per8, int nb_e, int nb_q, int q0, unsigned epoch, unsigned long long timeout) {
-    extern __shared__ double lct[];
-    const int b = (int)blockIdx.x;
-    if (b >= nb_e + nb_q) {
-        rf_reach_tile<MODE>(m, p, Y, dy, dg, p.rf_tile[b - nb_e - nb_q], nb_e, epoch, timeout);
-        return;
-    }
-    int eb = b;
-    const int qb = qd_split(b, nb_q, q0, &eb);
-    if (qb >= 0) {
-        const int r = qb * kEleBS + (int)threadIdx.x;
-        if (r < p.nqd) qd_pre<MODE, false, !(SHUD_RF_DIAG & 4)>(m, p, Y, r, 0, nullptr);
-        rf_publish(p.rf_flag + nb_e + qb, epoch);
-        return;
-    }
-    const int t = tile_of(per8, eb);
-    const int i = t * kEleBS + (int)threadIdx.x;
-    const bool act = i < n_compute;
-    const DevLake lk{};
-    double tv[kTabBatch];
-    tab_issue<kEleBS>(p, tv);
-    OwnRec own;
-    if (act) own = load_own<FU1, false>(p, Y, i, cur);
-    tab_store<kEleBS>(p, tv, lct);
-    unsigned *cnt = (unsigned *)(lct + p.ntab + (LSPK ? kLspN * kEleBS + kEleBS / 2 : 0));   // after the tables / slots
-    if ((SHUD_RF_DIAG & 8) && threadIdx.x == 0) *cnt = 0u;
-    if (p.rf_dbg_ticks && t == p.rf_dbg_tile && threadIdx.x == 0) {   // test hook: a late element tile
-        const unsigned long long t0 = wall_clock64();
-        while (wall_clock64() - t0 < p.rf_dbg_ticks) __builtin_amdgcn_s_sleep(8);
-    }
-    __syncthreads();
-    if (act) ele_body<MODE, OPEN, false, FU1, true, false, false, 0, LSPK, !(SHUD_RF_DIAG & 4)>(m, p, Y, dy, i, cur, dg, lk,
-                                                                                              lct, own);
-    if (SHUD_RF_DIAG & 8) rf_publish_lds(p.rf_flag + t, epoch, cnt);
-    else rf_publish(p.rf_flag + t, epoch);
 }
 
 template <int SB, bool QD>
@@ -1220,33 +1102,6 @@ void launch_copy_f64(double *dst, const double *src, size_t n, hipStream_t s) {
     if (!n) return;
     const size_t nb = std::min<size_t>((n + 255) / 256, 4096);
     hipLaunchKernelGGL(shud_copy_f64_kernel, dim3((unsigned)nb), dim3(256), 0, s, dst, src, n);
-}
-
-bool launch_rhs_packed_rf(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int n, int cur, int mode,
-                          bool open, bool fu_unit, const DevDiag &dg, unsigned epoch, unsigned long long timeout,
-                          hipStream_t s) {
-    if (n <= 0 || p.rf_ntile <= 0 || !p.rf_flag || !p.qdown || p.nqd <= 0 || p.ncls > LDS_CLS_MAX || p.nh ||
-        Y.gele || Y.griv)
-        return false;
-    const EleGrid g = ele_grid(n, p.nqd, p.rf_qd_pm);
-    const bool lsp = lds_bytes(p, true, true) + 16 <= kLspLdsMax;
-    const size_t lds = lds_bytes(p, true, lsp) + 16;                 // + the workgroup's publish counter
-    const dim3 grid(g.nb_e + g.nb_q + p.rf_ntile), blk(kEleBS);
-#define RF(MO, OP, FU) do {                                                                                      \
-        if (lsp) hipLaunchKernelGGL((shud_rhs_kernel_packed_rf<MO, OP, FU, 1>), grid, blk, lds, s, m, p, Y, dy, n,  \
-                                    cur, dg, g.per8(), g.nb_e, g.nb_q, g.q0, epoch, timeout);                    \
-        else hipLaunchKernelGGL((shud_rhs_kernel_packed_rf<MO, OP, FU, 0>), grid, blk, lds, s, m, p, Y, dy, n, cur, \
-                                dg, g.per8(), g.nb_e, g.nb_q, g.q0, epoch, timeout);                             \
-    } while (0)
-    if (mode == 0) {
-        if (open) { if (fu_unit) RF(0, true, true); else RF(0, true, false); }
-        else { if (fu_unit) RF(0, false, true); else RF(0, false, false); }
-    } else {
-        if (open) { if (fu_unit) RF(1, true, true); else RF(1, true, false); }
-        else { if (fu_unit) RF(1, false, true); else RF(1, false, false); }
-    }
-#undef RF
-    return true;
 }
 
 void launch_pack_step_kernel(const DevMesh &m, const DevPacked &p, int n, int cur, unsigned what, hipStream_t s) {

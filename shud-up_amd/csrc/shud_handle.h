@@ -57,11 +57,6 @@ struct shud_rhs {
     int n_classes = 0;
     bool fu_unit[2] = {true, true};      // fu_Surf / fu_Sub are all 1.0 (cryosphere off): not read
     bool qd_now = false;                 // this eval's element launch wrote DevPacked::qdown (river kernel reads it)
-    // river fold (build_river_fold): the eval's flag value (never 0), the reach tiles' poll bound, whether the last
-    // ordinary eval took the folded launch (its element-kernel time then includes the reaches)
-    unsigned rf_epoch = 0;
-    unsigned long long rf_timeout = 0;
-    bool rf_now = false;
 
     // host-pointer eval staging
     double *d_y = nullptr, *d_ydot = nullptr, *d_scratch_dy = nullptr;

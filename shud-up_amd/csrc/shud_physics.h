@@ -35,11 +35,7 @@ __device__ __forceinline__ double cdiv(double a, double b, double rb) {
 // in [2^-767, DBL_MAX] neither repair changes anything, so the bare chain gives the same bits (tests/test_kat.py::
 // test_fast_sqrt_div_bit_identical); any other x (zero, negative, tiny, inf, NaN) takes sqrt() on an exec-masked cold
 // path.  Saves the scaling compare/ldexp pair and the zero/inf select (~7 VALU) per call.
-#ifndef SHUD_SQRT_NR
-#define SHUD_SQRT_NR 0
-#endif
 __device__ __forceinline__ double sqrt_nr(double x) {
-#if SHUD_SQRT_NR
     const double y = __builtin_amdgcn_rsq(x);
     double g = x * y, h = y * 0.5;
     const double r = __builtin_fma(-h, g, 0.5);
@@ -51,18 +47,15 @@ __device__ __forceinline__ double sqrt_nr(double x) {
     g = __builtin_fma(d, h, g);
     if (__builtin_expect(!(x >= 0x1p-767 && x <= 0x1.fffffffffffffp+1023), 0)) g = sqrt(x);
     return g;
-#else
-    return sqrt(x);
-#endif
 }
 // division: LLVM's lowering is r = rcp(b') refined by two Newton steps, q = a' r, e = fma(-b', q, a'), q + e r (as
 // v_div_fmas), then v_div_fixup for special operands, where v_div_scale rescales a, b (a' , b') only when 1/b, a/b or a
 // would leave the normal range.  For |b| in [2^-100, 2^100] and |a| in [2^-900, 2^600] no operand is rescaled and
 // the fixup returns the quotient as is, so the bare chain gives the same bits; and r depends on b alone, so two
 // divisions by one divisor share it (Recip).  Other operands take the IEEE division on an exec-masked cold path.
-#ifndef SHUD_DIV_NR
-#define SHUD_DIV_NR 0
-#endif
+// Element kernel with both (sqrt_nr in satKfun, Manning and the weir; the two Dist2Nabor divisions of an edge and the
+// area divisions of the DY tail on shared reciprocals): wall per eval -0.5 % over 9 interleaved rounds, same bits
+// (profiles/r06/rf3/abv.log, lib:nr).
 struct Recip {
     double b, r;
     bool ok;                 // |b| in [2^-100, 2^100]
@@ -70,7 +63,6 @@ struct Recip {
 __device__ __forceinline__ Recip recip_nr(double b) {
     Recip R;
     R.b = b;
-#if SHUD_DIV_NR
     double r = __builtin_amdgcn_rcp(b);
     double e = __builtin_fma(-b, r, 1.0);
     r = __builtin_fma(r, e, r);
@@ -78,23 +70,15 @@ __device__ __forceinline__ Recip recip_nr(double b) {
     R.r = __builtin_fma(r, e, r);
     const double bb = __builtin_fabs(b);
     R.ok = bb >= 0x1p-100 && bb <= 0x1p100;
-#else
-    R.r = 0.;
-    R.ok = false;
-#endif
     return R;
 }
 __device__ __forceinline__ double div_nr(double a, const Recip &R) {
-#if SHUD_DIV_NR
     const double q0 = a * R.r;
     const double e = __builtin_fma(-R.b, q0, a);
     double q = __builtin_fma(e, R.r, q0);
     const double aa = __builtin_fabs(a);
     if (__builtin_expect(!(R.ok && aa >= 0x1p-900 && aa <= 0x1p600), 0)) q = a / R.b;
     return q;
-#else
-    return a / R.b;
-#endif
 }
 
 // ---- constants: src/Model/Macros.hpp:46-77 ----
@@ -110,50 +94,10 @@ __device__ __forceinline__ double div_nr(double a, const Recip &R) {
 // functions.hpp:117-123 (NOT fmin/fmax: NaN behaviour must match)
 __device__ __forceinline__ double rmin(double a, double b) { return (a > b ? b : a); }
 __device__ __forceinline__ double rmax(double a, double b) { return (a < b ? b : a); }
-// glibc's cbrt (sysdeps/ieee754/dbl-64/s_cbrt.c, glibc 2.35: the reference's libm for pow23's cbrt,
-// Equations.hpp:36-39) restated operation for operation: x = xm 2^xe with xm in [0.5, 1), a degree-6 polynomial u ~
-// xm^(1/3), one Halley step u (u^3 + 2 xm) / (2 u^3 + xm), times 2^((xe mod 3) / 3) from a 5-entry table, scaled by
-// 2^(xe / 3).  2 xm and 2 u^3 are exact, so t2 + 2 xm and 2 t2 + xm are single fmas with the same rounding; the Halley
-// quotient has numerator and denominator in [0.7, 3], where the bare division chain (div_nr's, without v_div_scale /
-// v_div_fixup) is the IEEE quotient.  Zero, infinite and NaN x return x + x, as glibc does.  Bit-identical to glibc's
-// cbrt (tests/test_kat.py::test_cbrt_glibc_bit_identical), so Manning's R^(2/3) is the oracle's bit for bit.
-#ifndef SHUD_CBRT_GLIBC
-#define SHUD_CBRT_GLIBC 0
-#endif
-__device__ __forceinline__ double cbrt_glibc(double x) {
-    constexpr double kC2 = 1.2599210498948731648, kSqC2 = 1.5874010519681994748;   // 2^(1/3), 2^(2/3)
-    int xe;
-    const double xm = __builtin_frexp(__builtin_fabs(x), &xe);
-    double p = 0.784932344976639262 - 0.145263899385486377 * xm;
-    p = -1.83469277483613086 + p * xm;
-    p = 2.44693122563534430 + p * xm;
-    p = -2.11499494167371287 + p * xm;
-    p = 1.50819193781584896 + p * xm;
-    const double u = 0.354895765043919860 + p * xm;
-    const double t2 = u * u * u;
-    const double num = u * __builtin_fma(xm, 2.0, t2), den = __builtin_fma(t2, 2.0, xm);
-    double r = __builtin_amdgcn_rcp(den);                       // num / den: the division chain, no repairs
-    double e = __builtin_fma(-den, r, 1.0);
-    r = __builtin_fma(r, e, r);
-    e = __builtin_fma(-den, r, 1.0);
-    r = __builtin_fma(r, e, r);
-    double q = num * r;
-    e = __builtin_fma(-den, q, num);
-    q = __builtin_fma(e, r, q);
-    const int q3 = xe / 3, rem = xe - 3 * q3;                   // C's truncating / and %
-    const double f = rem == 0 ? 1.0 : rem == 1 ? kC2 : rem == 2 ? kSqC2 : rem == -1 ? 1.0 / kC2 : 1.0 / kSqC2;
-    const double ym = q * f;
-    const double res = __builtin_ldexp(x > 0.0 ? ym : -ym, q3);
-    return __builtin_isfpclass(x, 0x0003 | 0x0204 | 0x0060) ? x + x : res;    // NaN, +-inf, +-0
-}
-__device__ __forceinline__ double pow23(double x) {
-#if SHUD_CBRT_GLIBC
-    const double t = cbrt_glibc(x);
-#else
-    const double t = cbrt(x);
-#endif
-    return t * t;
-}
+// (glibc's cbrt restated for the device — bit-identical to the reference's libm, tests/test_kat.py — measured +1.9 %
+// on the element kernel's wall per eval against OCML's cbrt, profiles/r06/rf3/abv.log lib:nrcb: not used here; the
+// restatement lives in the KAT library, shud_kat.hip cbrt_glibc)
+__device__ __forceinline__ double pow23(double x) { const double t = cbrt(x); return t * t; }
 
 // Equations.hpp:54-63.  The reference's two branches differ only in the sqrt argument (S or -S) and a leading
 // -1.0 factor; IEEE multiplication and division round sign-symmetrically, so (-1.0*x)*A*p/n == -(x*A*p/n) bit

@@ -111,8 +111,6 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
                         const std::vector<int> &up_idx);
 
 static int build_lakes(shud_rhs *h, const ShudMeshSoA *m, const ShudPartition *part);
-static int build_river_fold(shud_rhs *h, const ShudMeshSoA *m, const std::vector<int> &up_off,
-                            const std::vector<int> &up_idx);
 static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, const ShudRhsOptions *opt,
                  const ShudPartition *part) {
     const int NE = m->num_ele, NR = m->num_riv, NS = m->num_seg;
@@ -346,7 +344,6 @@ static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, cons
 #undef UP
     if ((rc = build_packed(h, m, p, eflags, seg_off, up_off, up_idx))) return rc;
     if (h->lakeon && (rc = build_lakes(h, m, part))) return rc;
-    if (!part && (rc = build_river_fold(h, m, up_off, up_idx))) return rc;
     if ((rc = h->dalloc(&h->d_err, 1))) return rc;
     if ((rc = h->dalloc(&h->d_warn, (size_t)kWarnSlots * kWarnStride))) return rc;
     d.err = h->d_err;
@@ -360,6 +357,59 @@ static int build(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *p, cons
     if ((rc = h->dalloc(&h->d_scratch_dy, ny))) return rc;
     return 0;
 }
+
+// Distinct fixed-length tuples of 64-bit words (bit patterns: two doubles are the same key when their bits are), each
+// numbered in first-seen order: open addressing over a power-of-two slot table, the tuples stored flat.  The class
+// search below runs it over every element several times per handle (one pass per candidate hybrid field set), so it
+// avoids per-element heap keys (std::string keys of 144 B cost seconds at 10M elements).
+class TupleSet {
+  public:
+    explicit TupleSet(int k) : k_(k), slots_(1024, -1) {}     // k <= 32
+    int size() const { return (int)(words_.size() / k_); }
+    const uint64_t *tuple(int id) const { return &words_[(size_t)id * k_]; }
+    // id of the tuple at p (k 8-byte words, any type: copied as bits), inserted if new
+    int insert(const void *p) {
+        uint64_t t[32];
+        memcpy(t, p, (size_t)k_ * 8);
+        if ((size_t)(size() + 1) * 2 > slots_.size()) grow();
+        size_t j = hash(t) & (slots_.size() - 1);
+        for (;; j = (j + 1) & (slots_.size() - 1)) {
+            const int id = slots_[j];
+            if (id < 0) break;
+            if (!memcmp(tuple(id), t, (size_t)k_ * 8)) return id;
+        }
+        const int id = size();
+        slots_[j] = id;
+        words_.insert(words_.end(), t, t + k_);
+        return id;
+    }
+
+  private:
+    uint64_t hash(const uint64_t *t) const {
+        uint64_t h = 0x9e3779b97f4a7c15ull;
+        for (int q = 0; q < k_; q++) {                  // splitmix64 finaliser per word, chained
+            uint64_t x = t[q] + h;
+            x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+            x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+            h = x ^ (x >> 31);
+        }
+        return h;
+    }
+    void grow() {
+        std::vector<int> old;
+        old.swap(slots_);
+        slots_.assign(old.size() * 2, -1);
+        for (int id : old) {
+            if (id < 0) continue;
+            size_t j = hash(tuple(id)) & (slots_.size() - 1);
+            while (slots_[j] >= 0) j = (j + 1) & (slots_.size() - 1);
+            slots_[j] = id;
+        }
+    }
+    int k_;
+    std::vector<int> slots_;
+    std::vector<uint64_t> words_;
+};
 
 // Packed class layout (shud_dev.h DevPacked).  Returns 0 with h->packed set, 0 with h->packed clear when
 // the mesh does not qualify (the SoA kernel is used), or an error code.
@@ -398,7 +448,6 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     // distinct parameter tuples -> class ids
     std::vector<std::vector<double>> table;           // [class][field]
     std::vector<int> cls(NE);
-    std::unordered_map<std::string, int> ids;
     const double dep_default = 0.0002;
     auto prim = [&](int i, std::vector<double> &r) {
         r[CF_macD] = p->macD[i]; r[CF_macKsatH] = p->macKsatH[i]; r[CF_vAreaF] = p->geo_vAreaF[i];
@@ -411,33 +460,31 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     };
     // the distinct tuples of the fields outside `mask` (mask fields zeroed), counting stops past `cap`
     auto count_tuples = [&](uint32_t mask, int cap) {
-        std::unordered_map<std::string, int> seen;
+        TupleSet seen(CF_NPRIMARY);
         std::vector<double> r(CF_NPRIMARY);
-        for (int i = 0; i < NE && (int)seen.size() <= cap; i++) {
+        for (int i = 0; i < NE && seen.size() <= cap; i++) {
             prim(i, r);
             for (int f = 0; f < CF_NPRIMARY; f++)
                 if (mask >> f & 1) r[f] = 0.;
-            seen.emplace(std::string((const char *)r.data(), r.size() * sizeof(double)), 0);
+            seen.insert(r.data());
         }
-        return (int)seen.size();
+        return seen.size();
     };
     // classes of the fields outside `mask` (mask fields zeroed); false past 32768 classes
     auto build_classes = [&](uint32_t mask) {
         table.clear();
-        ids.clear();
+        TupleSet ids(CF_NPRIMARY);
         std::vector<double> r(CF_NPRIMARY);
         for (int i = 0; i < NE; i++) {
             prim(i, r);
             for (int f = 0; f < CF_NPRIMARY; f++)
                 if (mask >> f & 1) r[f] = 0.;
-            std::string k((const char *)r.data(), r.size() * sizeof(double));
-            auto it = ids.find(k);
-            if (it == ids.end()) {
-                if ((int)table.size() >= 32768) return false;
-                it = ids.emplace(k, (int)table.size()).first;
+            const int id = ids.insert(r.data());
+            if (id == (int)table.size()) {
+                if (id >= 32768) return false;
                 table.push_back(r);
             }
-            cls[i] = it->second;
+            cls[i] = id;
         }
         return true;
     };
@@ -458,28 +505,27 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
             count_tuples(streamable, kLdsClassMax) <= kLdsClassMax) {
             // base classes: the tuples of the fields that cannot be streamed; then, per streamable field, how many
             // (base class, value) pairs it makes — the fields that split the base classes most are streamed first
-            std::unordered_map<std::string, int> bid;
+            TupleSet bid(CF_NPRIMARY);
             std::vector<int> base(NE);
             std::vector<double> r(CF_NPRIMARY);
             for (int i = 0; i < NE; i++) {
                 prim(i, r);
                 for (int f = 0; f < CF_NPRIMARY; f++)
                     if (streamable >> f & 1) r[f] = 0.;
-                base[i] = bid.emplace(std::string((const char *)r.data(), r.size() * sizeof(double)),
-                                      (int)bid.size()).first->second;
+                base[i] = bid.insert(r.data());
             }
             std::vector<std::pair<size_t, int>> split;       // (distinct (base, value) pairs, field)
             for (int f = 0; f < CF_NPRIMARY; f++) {
                 if (!(streamable >> f & 1)) continue;
-                std::unordered_map<std::string, int> pairs;
-                for (int i = 0; i < NE && pairs.size() <= (size_t)1 << 20; i++) {
+                TupleSet pairs(2);                           // (base class, field value bits)
+                for (int i = 0; i < NE && pairs.size() <= 1 << 20; i++) {
                     prim(i, r);
-                    char key[12];
-                    memcpy(key, &base[i], 4);
-                    memcpy(key + 4, &r[f], 8);
-                    pairs.emplace(std::string(key, 12), 0);
+                    uint64_t key[2];
+                    key[0] = (uint64_t)base[i];
+                    memcpy(&key[1], &r[f], 8);
+                    pairs.insert(key);
                 }
-                if (pairs.size() > bid.size()) split.push_back({pairs.size(), f});
+                if (pairs.size() > bid.size()) split.push_back({(size_t)pairs.size(), f});
             }
             std::stable_sort(split.begin(), split.end(),
                              [](const std::pair<size_t, int> &a, const std::pair<size_t, int> &b) {
@@ -666,73 +712,6 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     P.qd_pm_fold = env_knob("SHUD_QD_POS_FOLD", 1000, 0, 1000);
     h->n_classes = ncls;
     h->packed = true;
-    return 0;
-}
-
-// River fold (DevPacked::rf_*, shud_ele_packed.hip shud_rhs_kernel_packed_rf): the reaches ride in the last blocks of
-// the element launch.  Per reach tile (256 reaches, the river kernel's tiles): the element tiles owning any segment of
-// every 128-B qseg2 line its segment gathers touch (whole lines: no reach tile ever caches a line another element tile
-// has yet to write), and the QrivDown blocks of its own and upstream reaches — each a contiguous range (band-numbered
-// meshes: syn-10M spans <= 99 element tiles and <= 11 QrivDown blocks).  River blocks are dealt to reach tiles in the
-// order their inputs come due: by the latest launch block among those they wait for.  Unpartitioned, lake-free
-// handles on the LDS class table only; SHUD_RHS_RFOLD=1 (measured slower so far, DESIGN §4 round 6: opt-in).
-static int build_river_fold(shud_rhs *h, const ShudMeshSoA *m, const std::vector<int> &up_off,
-                            const std::vector<int> &up_idx) {
-    DevPacked &P = h->dp;
-    const int nor = h->n_own_riv, NS = m->num_seg, n = h->n_own + h->n_segghost;
-    if (!h->packed || h->lakeon || h->partitioned || nor <= 0 || !P.qdown || P.nqd <= 0 || P.nh ||
-        P.ncls > kLdsClassMax || !env_knob("SHUD_RHS_RFOLD", 0, 0, 1))
-        return 0;
-    P.rf_qd_pm = env_knob("SHUD_QD_POS_RF", 0, 0, 1000);
-    const EleGrid g = ele_grid(n, P.nqd, P.rf_qd_pm);
-    const int ntile = (nor + 255) / 256, nl = (NS + 7) / 8;
-    // element tile range of every 128-B line of qseg2 (element-sorted positions, 8 per line)
-    std::vector<int> lmin(nl, INT_MAX), lmax(nl, -1), pos_of(NS);
-    for (int k = 0; k < NS; k++) {
-        const int t = m->seg_ele[h->seg_perm[k]] / 256;
-        pos_of[h->seg_perm[k]] = k;
-        lmin[k / 8] = std::min(lmin[k / 8], t);
-        lmax[k / 8] = std::max(lmax[k / 8], t);
-    }
-    std::vector<int4> dep(ntile);
-    for (int j = 0; j < ntile; j++) dep[j] = make_int4(INT_MAX, -1, j, j);   // own reaches: QrivDown block j
-    for (int s = 0; s < NS; s++) {
-        const int r = m->seg_riv[s];
-        if (r >= nor) continue;
-        const int l = pos_of[s] / 8;
-        int4 &d = dep[r / 256];
-        d.x = std::min(d.x, lmin[l]);
-        d.y = std::max(d.y, lmax[l]);
-    }
-    for (int r = 0; r < nor; r++)
-        for (int k = up_off[r]; k < up_off[r + 1]; k++) {
-            int4 &d = dep[r / 256];
-            d.z = std::min(d.z, up_idx[k] / 256);
-            d.w = std::max(d.w, up_idx[k] / 256);
-        }
-    std::vector<std::pair<long long, int>> due(ntile);
-    for (int j = 0; j < ntile; j++) {
-        int4 &d = dep[j];
-        if (d.y < 0) { d.x = 0; d.y = -1; }                  // no segments: QrivDown blocks only
-        long long key = -1;
-        for (int t = d.x; t <= d.y; t++) key = std::max<long long>(key, g.block_of_tile(t));
-        for (int q = d.z; q <= d.w; q++) key = std::max<long long>(key, g.block_of_qd(q));
-        due[j] = {key, j};
-    }
-    std::stable_sort(due.begin(), due.end());
-    std::vector<int> order(ntile);
-    for (int j = 0; j < ntile; j++) order[j] = due[j].second;
-    int rc;
-    unsigned *flag_d; int *tile_d; int4 *dep_d;
-    if ((rc = h->upload(&flag_d, (const unsigned *)nullptr, (size_t)g.nb_e + g.nb_q))) return rc;
-    if ((rc = h->upload(&tile_d, order.data(), ntile))) return rc;
-    if ((rc = h->upload(&dep_d, dep.data(), ntile))) return rc;
-    P.rf_flag = flag_d; P.rf_tile = tile_d; P.rf_dep = dep_d; P.rf_ntile = ntile;
-    h->rf_epoch = 0;
-    int khz = 0;
-    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device) == hipSuccess && khz > 0)
-        h->wall_khz = khz;
-    h->rf_timeout = (unsigned long long)(env_knob("SHUD_HALO_TIMEOUT_MS", 5000, 1, 3600000) * h->wall_khz);
     return 0;
 }
 
@@ -1093,19 +1072,6 @@ static int launch_split(shud_rhs *h, const double *y, double *dy, hipEvent_t e_m
         launch_riv(h, y, dy, false);
     } else {
         if (h->partitioned) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_comm, 0));
-        if (h->dp.rf_ntile > 0 && !h->partitioned) {          // river fold: one launch (build_river_fold)
-            YView Y{y, h->d_gele, h->d_griv, h->n_own, h->n_own_riv};
-            if (++h->rf_epoch == 0) h->rf_epoch = 1;
-            if (launch_rhs_packed_rf(h->dm, h->dp, Y, dy, h->n_own + h->n_segghost, h->cur, h->mode, h->open,
-                                     h->fu_unit[0] && h->fu_unit[1], h->dd, h->rf_epoch, h->rf_timeout, h->stream)) {
-                h->qd_now = true;
-                h->rf_now = true;
-                if (e_mid) HIP_TRY(hipEventRecord(e_mid, h->stream));
-                HIP_TRY(hipGetLastError());
-                return 0;
-            }
-        }
-        h->rf_now = false;
         launch_ele(h, y, dy, h->cur, h->cur_e, false);
         if (e_mid) HIP_TRY(hipEventRecord(e_mid, h->stream));
         launch_riv(h, y, dy, false);
@@ -1156,12 +1122,6 @@ extern "C" long long shud_rhs_num_calls(shud_rhs_t h) { return h ? h->ncalls : -
 extern "C" int shud_rhs_layout_streamed(shud_rhs_t h, int *n_streamed) {
     if (!h || !n_streamed) return shud_fail(SHUD_ERR_ARG, "null argument");
     *n_streamed = h->packed ? h->dp.nh : 0;
-    return SHUD_OK;
-}
-
-extern "C" int shud_rhs_layout_river_fold(shud_rhs_t h, int *folded) {
-    if (!h || !folded) return shud_fail(SHUD_ERR_ARG, "null argument");
-    *folded = h->dp.rf_ntile > 0 ? 1 : 0;
     return SHUD_OK;
 }
 
@@ -1374,27 +1334,6 @@ extern "C" int shud_rhs_debug_halo(shud_rhs_t h, double spin_us, const double *d
     h->dbg_armed = h->dbg_spin || d_ele_src || d_riv_src || !h->dbg_publish;
     const double ms = timeout_ms > 0 ? timeout_ms : env_knob("SHUD_HALO_TIMEOUT_MS", 5000, 1, 3600000);
     h->halo_timeout = (unsigned long long)(ms * h->wall_khz);
-    return SHUD_OK;
-}
-extern "C" int shud_rhs_debug_rfold(shud_rhs_t h, int tile, double spin_us, double timeout_ms, int *tile_out) {
-    if (!h || h->dp.rf_ntile <= 0) return shud_fail(SHUD_ERR_ARG, "not a river-folded handle");
-    if (spin_us < 0 || spin_us > 1e7) return shud_fail(SHUD_ERR_ARG, "spin_us out of range");
-    HIP_TRY(hipSetDevice(h->device));
-    HIP_TRY(hipStreamSynchronize(h->stream));
-    const EleGrid g = ele_grid(h->n_own + h->n_segghost, h->dp.nqd, h->dp.rf_qd_pm);
-    if (tile < 0) {                                   // the element tile the most reach tiles wait for
-        std::vector<int4> dep(h->dp.rf_ntile);
-        HIP_TRY(hipMemcpy(dep.data(), h->dp.rf_dep, dep.size() * sizeof(int4), hipMemcpyDeviceToHost));
-        std::vector<int> cnt(g.nb_e, 0);
-        for (const int4 &d : dep)
-            for (int t = d.x; t <= d.y; t++) cnt[t]++;
-        tile = (int)(std::max_element(cnt.begin(), cnt.end()) - cnt.begin());
-    }
-    if (tile >= g.nb_e) return shud_fail(SHUD_ERR_ARG, "tile %d out of range (%d element tiles)", tile, g.nb_e);
-    h->dp.rf_dbg_tile = tile;
-    h->dp.rf_dbg_ticks = (unsigned long long)(spin_us * 1e-3 * h->wall_khz);
-    if (timeout_ms > 0) h->rf_timeout = (unsigned long long)(timeout_ms * h->wall_khz);
-    if (tile_out) *tile_out = tile;
     return SHUD_OK;
 }
 // split eval for external transport: pack, (caller exchanges), compute

@@ -169,7 +169,6 @@ FUNCTIONS = {
     "shud_rhs_num_calls": (C.c_longlong, [_H]),
     "shud_rhs_layout": (C.c_int, [_H, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "shud_rhs_layout_streamed": (C.c_int, [_H, C.POINTER(C.c_int)]),
-    "shud_rhs_layout_river_fold": (C.c_int, [_H, C.POINTER(C.c_int)]),
     "shud_rhs_destroy": (C.c_int, [_H]),
     "shud_rhs_last_error_string": (C.c_char_p, []),
     "shud_rhs_cvrhs": (C.c_int, [C.c_double, C.c_void_p, C.c_void_p, C.c_void_p]),
@@ -191,7 +190,6 @@ FUNCTIONS = {
     "shud_rhs_eval_pack": (C.c_int, [_H, C.c_void_p]),
     "shud_rhs_eval_compute": (C.c_int, [_H, C.c_double, C.c_void_p, C.c_void_p]),
     "shud_rhs_debug_halo": (C.c_int, [_H, C.c_double, C.c_void_p, C.c_void_p, C.c_int, C.c_double]),
-    "shud_rhs_debug_rfold": (C.c_int, [_H, C.c_int, C.c_double, C.c_double, C.POINTER(C.c_int)]),
 }
 # include/shud_et.h
 ET_FUNCTIONS = {

@@ -120,10 +120,6 @@ class RhsHandle:
         out = {"packed": bool(pk.value), "n_classes": nc.value}
         if ns.value:
             out["streamed_fields"] = ns.value
-        rf = C.c_int()
-        _check(lib().shud_rhs_layout_river_fold(self.h, C.byref(rf)), "shud_rhs_layout_river_fold")
-        if rf.value:
-            out["river_fold"] = True
         return out
 
     def diagnostics(self):
@@ -240,13 +236,6 @@ class RhsHandle:
 
     def eval_compute(self, t, d_y, d_ydot):
         _check(lib().shud_rhs_eval_compute(self.h, float(t), C.c_void_p(d_y), C.c_void_p(d_ydot)), "eval_compute")
-
-    def debug_rfold(self, tile=-1, spin_us=0.0, timeout_ms=0.0):
-        """test hook (shud_rhs_debug_rfold): a late element tile in the river-folded launch; returns the tile armed"""
-        t = C.c_int()
-        _check(lib().shud_rhs_debug_rfold(self.h, int(tile), float(spin_us), float(timeout_ms), C.byref(t)),
-               "debug_rfold")
-        return t.value
 
     def debug_halo(self, spin_us=0.0, d_ele_src=None, d_riv_src=None, publish=True, timeout_ms=0.0):
         """test hook (shud_rhs_debug_halo): late / kernel-written / missing halo on the comm stream"""

@@ -27,8 +27,7 @@ def per_kernel(d, counter):
             continue
         n = r["Kernel_Name"]
         key = ("shud_ele_kernel" if "ele_kernel" in n else "shud_riv_kernel" if "riv_kernel" in n else
-               "shud_rhs_kernel_rf" if "rhs_kernel_packed_rf" in n else "shud_pack_kernel" if "pack_kernel" in n else
-               None)
+               "shud_pack_kernel" if "pack_kernel" in n else None)
         if key:
             agg.setdefault(key, []).append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in agg.items()}
@@ -41,8 +40,7 @@ def per_kernel(d, counter):
 # rounds 1-3 streamed a 48-B segment record)
 # river kernel: its 64-B record, the 16-B index word rv_u, stage 8 per reach (round 4; rounds 1-3 also rv_i 16);
 # segment positions 4 per segment.
-# river fold (round 6): one launch holds both (shud_rhs_kernel_packed_rf).
-COALESCED = {"shud_ele_kernel": (164, 0, 20), "shud_riv_kernel": (0, 88, 4), "shud_rhs_kernel_rf": (164, 88, 24)}
+COALESCED = {"shud_ele_kernel": (164, 0, 20), "shud_riv_kernel": (0, 88, 4)}
 
 
 def main():
