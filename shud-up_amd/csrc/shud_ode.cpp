@@ -30,11 +30,9 @@
 #include "shud_ode.h"
 #include "shud_ode_dev.h"
 
-// SHUD_ODE_SPIN (default): a fetch polls the last finalize's completion word in host-mapped memory instead of
-// blocking in hipStreamSynchronize (0: synchronize; A/B 4.39 vs 4.43 ms per step, profiles/r04/ode_spin/)
-#ifndef SHUD_ODE_SPIN
-#define SHUD_ODE_SPIN 1
-#endif
+// A fetch polls the last finalize's completion word in host-mapped memory instead of blocking in
+// hipStreamSynchronize (A/B 4.39 vs 4.43 ms per step, profiles/r04/ode_spin/).  The round 3-5 A/B switches of this
+// file (synchronize-only fetches, eager cvCompleteStep, stored zn[0]) were removed in round 6; commit a4b4e96 holds them.
 
 using namespace shud::ode;
 
@@ -46,17 +44,8 @@ constexpr double ADDON = 0.000001, BIAS1 = 6.0, BIAS2 = 6.0, BIAS3 = 10.0, ONEPS
 constexpr int SMALL_NST = 10, MXNCF = 10, MXNEF = 7, MXNEF1 = 3, SMALL_NEF = 2, LONG_WAIT = 10, MSBP = 20;
 constexpr double DGMAX = 0.3, CRDOWN = 0.3, RDIV = 2.0, NLSCOEF = 0.1;
 constexpr int NLS_MAXCOR = 3;
-// SHUD_ODE_LAZY_COMPLETE=0: cvCompleteStep updates all of zn[0..q] in its own pass (A/B); default: zn[0] at once,
-// zn[1..q] deferred into the next predict (ode::Pend)
-#ifndef SHUD_ODE_LAZY_COMPLETE
-#define SHUD_ODE_LAZY_COMPLETE 1
-#endif
-constexpr bool kLazyComplete = SHUD_ODE_LAZY_COMPLETE != 0;
-// SHUD_ODE_LAZY_ZN0=0: the complete+ewt pass stores zn[0] (only zn[1..q] deferred; A/B)
-#ifndef SHUD_ODE_LAZY_ZN0
-#define SHUD_ODE_LAZY_ZN0 1
-#endif
-constexpr int kLazyZn0 = SHUD_ODE_LAZY_ZN0 != 0;
+// cvCompleteStep: its pass forms zn[0]'s new value for the next error weights without storing it; zn[0..q] and the
+// acor copy are deferred into the next predict (ode::Pend; 4.48 vs 4.58 ms per step eager, profiles/r04/ode_lazy_*)
 constexpr double CVLS_EPLIN = 0.05, CVLS_DGMAX = 0.2;
 constexpr int CVLS_MSBJ = 51;
 enum { FIRST_CALL = 0, PREV_CONV_FAIL = 1, PREV_ERR_FAIL = 2 };
@@ -135,7 +124,6 @@ struct shud_ode {
     // memory (shud_ode_kernels.hip k_finalize), so a fetch is one stream synchronize
     bool fetch() {
         hipError_t e = hipSuccess;
-#if SHUD_ODE_SPIN
         // poll the last enqueued finalize's completion word (host-mapped, coherent) instead of blocking in the
         // runtime; after ~2 s, or with no finalize yet, synchronize (which also reports a device fault)
         bool done = false;
@@ -149,9 +137,6 @@ struct shud_ode {
             }
         }
         if (!done) e = hipStreamSynchronize(s);
-#else
-        e = hipStreamSynchronize(s);
-#endif
         if (e == hipSuccess) e = hipGetLastError();
         n_sync++;
         if (e != hipSuccess) {
@@ -613,18 +598,14 @@ struct shud_ode {
             indx_acor = qmax;
         }
         // cvCompleteStep + the next loop iteration's cvEwtSet / N_VWrmsNorm(zn[0]) in one pass (ewt_and_norm);
-        // SHUD_ODE_LAZY_COMPLETE: that pass completes zn[0] only, zn[1..q] and the acor copy ride in the next predict
-        if (kLazyComplete) {
-            complete_step_ewt(n, zn, acor, lc, 0, -1, kLazyZn0, rtol, atol, ewt_alt, rs(S_EWTMIN), s);
-            pend = ode::Pend{};
-            pend.acor = acor;
-            pend.l = lc;
-            pend.q = q;
-            pend.copy_to = copy_to;
-            pend.j0 = kLazyZn0 ? 0 : 1;
-        } else {
-            complete_step_ewt(n, zn, acor, lc, q, copy_to, 0, rtol, atol, ewt_alt, rs(S_EWTMIN), s);
-        }
+        // that pass completes nothing in memory: zn[0..q] and the acor copy ride in the next predict (ode::Pend)
+        complete_step_ewt(n, zn, acor, lc, 0, -1, 1, rtol, atol, ewt_alt, rs(S_EWTMIN), s);
+        pend = ode::Pend{};
+        pend.acor = acor;
+        pend.l = lc;
+        pend.q = q;
+        pend.copy_to = copy_to;
+        pend.j0 = 0;
         fin(S_EWTMIN, 2, 1u);
         ewt_pending = true;
         ewt_fin_sync = n_sync;

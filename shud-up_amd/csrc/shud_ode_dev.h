@@ -107,7 +107,7 @@ void normalize(int64_t n, double *w, double c, const double *ewt, const Red &r, 
 // ycor += delta; r: [sum (delta*ewt)^2, sum (ycor*ewt)^2]
 void newton_update(int64_t n, const double *V, int64_t vstride, int krydim, const Coefs &yg, const double *dsrc,
                    const double *ewt, double *ycor, bool ycor_zero, const Red &r, hipStream_t s);
-// 1 when predict() leaves ycor unwritten (SHUD_ODE_LAZY_YCOR): the caller then passes ycor_zero until the first
+// 1: predict() leaves ycor unwritten: the caller then passes ycor_zero until the first
 // newton_update after a predict
 int lazy_ycor();
 // zn[j] = l[j]*acor + zn[j], j = jlo..q; if copy_to >= 0: zn[copy_to] = acor

@@ -29,23 +29,10 @@ static int ew_blocks(int64_t n) {
 // single-use streams: non-temporal loads and stores (global_load/store ... nt).  The vectors are NY-long (250 MB
 // at syn-10M), far beyond L2; nt loads+stores measured 7 % faster on the five-operand pass
 // (profiles/r03/ode/ode_red_bench.log)
-// SHUD_ODE_NT: bit 0 non-temporal loads, bit 1 non-temporal stores (A/B builds, tools/ablib.sh -tu ode)
-#ifndef SHUD_ODE_NT
-#define SHUD_ODE_NT 3
-#endif
-#ifndef SHUD_ODE_LAZY_YCOR
-#define SHUD_ODE_LAZY_YCOR 1
-#endif
 template <class T>
-__device__ __forceinline__ T ldn(const T *p) {
-    if (SHUD_ODE_NT & 1) return __builtin_nontemporal_load(p);
-    return *p;
-}
+__device__ __forceinline__ T ldn(const T *p) { return __builtin_nontemporal_load(p); }
 template <class T>
-__device__ __forceinline__ void stn(T *p, T v) {
-    if (SHUD_ODE_NT & 2) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
+__device__ __forceinline__ void stn(T *p, T v) { __builtin_nontemporal_store(v, p); }
 
 // One entry per thread: use(i, load(i)) for i = block * BS + thread when i < n (BS = blockDim.x).  Reductions run
 // on the full one-shot grid (ceil(n / kRedThreads) blocks) rather than a grid-stride loop: the grid-stride form
@@ -188,14 +175,13 @@ void ewt_set(int64_t n, const double *zn0, double *ewt, double rtol, double atol
 // cvPredict with y != null also performs the next cvNls start (every predict is followed by one): ycor = 0
 // (N_VConst) and y = zn[0] + ycor (N_VLinearSum) on the new zn[0] — the same add as k_vsum_zero, so -0.0
 // becomes +0.0 exactly as there — saving that pass's re-read of zn[0] (+8 B/entry here, -24 B/entry there).
-// SHUD_ODE_LAZY_YCOR (default): the ycor = 0 fill is not stored at all — the controller marks ycor "all +0.0"
+// The ycor = 0 fill is not stored at all — the controller marks ycor "all +0.0"
 // and its only readers before the first Newton update (k_residual, k_newton_update) take the zeros as operands
 // instead of loading them (identical values; -8 B/entry here and in that k_newton_update)
 // PEND (cvPredict after a deferred cvCompleteStep, Pend): zn[j] = l[j]*acor + zn[j] and zn[j] *= r[j] (j = 1..Q) in
 // registers first — k_complete's and k_rescale's arithmetic — then the Pascal update; zn[Q] is stored too, and
 // zn[copy_to] = acor.  Saves the completion's own pass over zn[1..Q] (+16 B/entry here, -16*Q B/entry there).
-// ycor is not __restrict__: predict_pend passes acor as both ycor and pd.acor, and the eager-fill A/B build
-// (SHUD_ODE_LAZY_YCOR=0) stores ycor[i] after loading pd.acor[i] (the default build never stores ycor)
+// ycor is not __restrict__: predict_pend passes acor as both ycor and pd.acor (it is never stored here)
 template <int Q, bool FWD, bool PEND, int U>
 __global__ void __launch_bounds__(kThreads) k_pascal(int64_t n, double *__restrict__ zn, double *__restrict__ y,
                                                      double *ycor, Pend pd) {
@@ -228,7 +214,6 @@ __global__ void __launch_bounds__(kThreads) k_pascal(int64_t n, double *__restri
         }
         if (FWD && y) {
             const double zero = 0.0;
-            if (SHUD_ODE_LAZY_YCOR == 0) stn(ycor + i, zero);
             stn(y + i, a.v[0] + zero);
         }
     });
@@ -247,7 +232,7 @@ static void pascal(int64_t n, double *zn, int q, double *y, double *ycor, const 
     default: pascal_q<5, FWD, PEND>(n, zn, y, ycor, pd, s); break;
     }
 }
-int lazy_ycor() { return SHUD_ODE_LAZY_YCOR; }
+int lazy_ycor() { return 1; }
 void predict(int64_t n, double *zn, int q, double *y, double *ycor, hipStream_t s) {
     pascal<true, false>(n, zn, q, y, ycor, Pend{}, s);
 }

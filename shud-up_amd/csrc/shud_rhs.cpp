@@ -36,14 +36,10 @@ thread_local std::string g_last_error;
 
 // Event scopes.  Every event here orders work between queues of one device (the comm stream's pack / exchange and
 // the main stream's kernels) or times kernels: a device-scope release is enough for both, and the default
-// system-scope release writes the L2's dirty lines back to HBM at every record (SHUD_EV_SCOPE=0: the HIP
-// defaults, A/B only).  RCCL's own kernels on s_comm complete before ev_comm, which then publishes their writes
-// to this device's other queues.
-#ifndef SHUD_EV_SCOPE
-#define SHUD_EV_SCOPE 1
-#endif
-static constexpr unsigned kEvSync = SHUD_EV_SCOPE ? hipEventDisableSystemFence : 0u;
-static constexpr unsigned kEvTime = SHUD_EV_SCOPE ? hipEventReleaseToDevice : hipEventDefault;
+// system-scope release writes the L2's dirty lines back to HBM at every record (profiles/r03/ev_scope/).  RCCL's
+// own kernels on s_comm complete before ev_comm, which then publishes their writes to this device's other queues.
+static constexpr unsigned kEvSync = hipEventDisableSystemFence;
+static constexpr unsigned kEvTime = hipEventReleaseToDevice;
 
 int shud_fail(int code, const char *fmt, ...) {
     char buf[512];
