@@ -14,7 +14,7 @@ using namespace shud;
 // quotient has numerator and denominator in [0.7, 3], where the bare division chain (div_nr's, without v_div_scale /
 // v_div_fixup) is the IEEE quotient.  Zero, infinite and NaN x return x + x, as glibc does.  Bit-identical to glibc's
 // cbrt (tests/test_kat.py::test_cbrt_glibc_bit_identical).  Not in the kernels: +1.9 % wall per eval against OCML's cbrt
-// in the element kernel (profiles/r06/rf3/abv.log, lib:nrcb), so Manning keeps OCML's cbrt (within the parity tolerance).
+// in the element kernel (profiles/r06/rfold/abv_fold_sqrt_div_cbrt.log, lib:nrcb), so Manning keeps OCML's cbrt (within the parity tolerance).
 __device__ __forceinline__ double cbrt_glibc(double x) {
     constexpr double kC2 = 1.2599210498948731648, kSqC2 = 1.5874010519681994748;   // 2^(1/3), 2^(2/3)
     int xe;

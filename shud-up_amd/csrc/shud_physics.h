@@ -55,7 +55,7 @@ __device__ __forceinline__ double sqrt_nr(double x) {
 // divisions by one divisor share it (Recip).  Other operands take the IEEE division on an exec-masked cold path.
 // Element kernel with both (sqrt_nr in satKfun, Manning and the weir; the two Dist2Nabor divisions of an edge and the
 // area divisions of the DY tail on shared reciprocals): wall per eval -0.5 % over 9 interleaved rounds, same bits
-// (profiles/r06/rf3/abv.log, lib:nr).
+// (profiles/r06/rfold/abv_fold_sqrt_div_cbrt.log, lib:nr).
 struct Recip {
     double b, r;
     bool ok;                 // |b| in [2^-100, 2^100]
@@ -95,8 +95,8 @@ __device__ __forceinline__ double div_nr(double a, const Recip &R) {
 __device__ __forceinline__ double rmin(double a, double b) { return (a > b ? b : a); }
 __device__ __forceinline__ double rmax(double a, double b) { return (a < b ? b : a); }
 // (glibc's cbrt restated for the device — bit-identical to the reference's libm, tests/test_kat.py — measured +1.9 %
-// on the element kernel's wall per eval against OCML's cbrt, profiles/r06/rf3/abv.log lib:nrcb: not used here; the
-// restatement lives in the KAT library, shud_kat.hip cbrt_glibc)
+// on the element kernel's wall per eval against OCML's cbrt, profiles/r06/rfold/abv_fold_sqrt_div_cbrt.log lib:nrcb:
+// not used here; the restatement lives in the KAT library, shud_kat.hip cbrt_glibc)
 __device__ __forceinline__ double pow23(double x) { const double t = cbrt(x); return t * t; }
 
 // Equations.hpp:54-63.  The reference's two branches differ only in the sqrt argument (S or -S) and a leading
