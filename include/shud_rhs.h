@@ -189,6 +189,9 @@ int  shud_rhs_layout(shud_rhs_t h, int *packed, int *n_classes);
  * depression, Rough) are streamed per element because the full parameter tuples exceed one workgroup's LDS class
  * table (per-element-calibrated models); 0 = every field from the class table */
 int  shud_rhs_layout_streamed(shud_rhs_t h, int *n_streamed);
+/* in-tile edge sharing of a packed handle: *n_shared interior edges are evaluated once and read by the other element
+ * of the edge (exactly antisymmetric pairs within one 256-element tile, single-GPU handles; SHUD_RHS_SHARE=0: off) */
+int  shud_rhs_layout_shared(shud_rhs_t h, int *n_shared);
 int  shud_rhs_destroy(shud_rhs_t h);
 const char *shud_rhs_last_error_string(void);
 

@@ -93,6 +93,9 @@ inline bool cdiv_divisor_ok(double b) {
 }
 // most classes one workgroup stages in LDS (128 x 27 x 8 B = 27 KiB)
 constexpr int kLdsClassMax = 128;
+// elements per workgroup of the packed element kernel (shud_ele_packed.hip kEleBS): the tiles the host's edge-sharing
+// assignment (shud_rhs.cpp, seg_first bits 26-29) pairs elements within
+constexpr int kShareTile = 256;
 // pow_tab's log + exp tables (shud_pow_tab.h: 256 x 4 + 128 x 2 doubles; SHUD_PT_COMPACT: 128 x 2.5 + 128 x 2), staged in
 // LDS after the class table (shud_rhs.cpp checks the sizes against the generated tables)
 #ifndef SHUD_PT_COMPACT

@@ -86,7 +86,22 @@ constexpr int CF_LDS_STRIDE = CF_STRIDE;   // the HBM table's record layout, cop
 // (MD_f.cpp:146-150); bank edges of other elements exchange with the lake (MD_ElementFlux.cpp:46-53,107-121)
 // and leave their fluxes in DevLake for the lake kernel.  LAKE = false compiles all of it away.
 constexpr int kEleWaves = 5;      // min waves per SIMD: <= 96 VGPRs (rolled edge loop, no spills)
+constexpr int kEleWavesSh = 7;    // the edge-sharing instantiations with the parked DY tail (kEleWavesOf)
+// in-tile edge sharing (ele_body, SH): the ghost-free, lake-free, non-hybrid, non-diagnostic instantiations with the
+// class table in LDS (the 256-thread ones; the 1024-thread table kernel passes BS = 1024)
+constexpr bool kShareOn(bool lct, bool gh, bool lake, int hyb, bool diag) {
+    return lct && !gh && !lake && hyb == 0 && !diag;
+}
+// min waves per SIMD of an instantiation: with sharing and the parked DY tail 7 (72 VGPRs, no spills with FU1; 6
+// without FU1, where 7 would spill), others 5
+constexpr int kEleWavesOf(bool lct, int lspk, bool gh, bool lake, int hyb, bool diag, bool fu1) {
+    return (kShareOn(lct, gh, lake, hyb, diag) && lspk) ? (fu1 ? kEleWavesSh : 6) : kEleWaves;
+}
 constexpr int kEleBS = 256;       // elements per workgroup
+static_assert(kEleBS == kShareTile, "edge sharing pairs elements within one workgroup's tile");
+static_assert(2 * kEleBS <= kPowTabDoubles, "edge-sharing slots fit the pow tables' LDS region");
+// an edge-sharing slot's "evaluate it yourself" mark: a signalling NaN, which no arithmetic result is
+constexpr uint64_t kShareVoid = 0x7ff0000000000001ull;
 // f_etFlux's three conditions (negative flux, NaN, eta > 2 ETP) are collected in a lane bit mask and reported together —
 // one ballot per wave when none fired (the common case) instead of three; the same flags, first indices and warning
 // count (atomics commute).  (Deferring all five conditions to the end of the body kept the mask live across the edge
@@ -180,7 +195,7 @@ __device__ __forceinline__ int qd_split(int b, int nb_q, int q0, int *e) {
     return -1;
 }
 
-template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB = 0, int LSP = 0>
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB = 0, int LSP = 0, int BS = 256>
 __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, const YView &Y, double *__restrict__ dy,
                                          int i, int cur, const DevDiag &dg, const DevLake &lk, const double *lct,
                                          const OwnRec &own);
@@ -199,7 +214,7 @@ constexpr size_t kLspLdsMax = 23296;
 // per-element record, the rest from the LDS class table; 1 = one streamed field (one 8-B value per element, held in
 // one register pair), 2 = two to four
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB = 0, int LSPK = 0>
-__global__ void __launch_bounds__(kEleBS, kEleWaves)
+__global__ void __launch_bounds__(kEleBS, kEleWavesOf(LCT, LSPK, GH, LAKE, HYB, DIAG, FU1))
 shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int i0, int n_compute, int cur,
                        DevDiag dg, DevLake lk, int per8, int nb_q, int q0) {
     extern __shared__ double lct[];                       // ntab doubles (class table + pow tables) when LCT
@@ -238,7 +253,7 @@ shud_ele_kernel_packed_big(DevMesh m, DevPacked p, YView Y, double *__restrict__
     if (act) own = load_own<FU1, GH>(p, Y, i, cur);
     tab_store<1024>(p, tv, lct);
     __syncthreads();
-    if (act) ele_body<MODE, OPEN, DIAG, FU1, true, false, GH>(m, p, Y, dy, i, cur, dg, lk, lct, own);
+    if (act) ele_body<MODE, OPEN, DIAG, FU1, true, false, GH, 0, 0, 1024>(m, p, Y, dy, i, cur, dg, lk, lct, own);
 }
 
 // Partitioned handles: one launch for the interior elements [0, n_int) (ghost-free instantiation, XCD-chunked
@@ -347,7 +362,7 @@ __device__ __forceinline__ void hload(const DevPacked &p, int i, double (&v)[4])
 // (Edge j+1's neighbour gathers issued at the top of edge j's iteration, or edge 0's before the segment loop: 92 / 94
 // VGPRs, 5 waves per SIMD, element kernel 0.620 / 0.627 vs 0.600 ms; forced to 6 waves it spills (0.752).  Occupancy
 // hides the gathers' latency better than the extra loads in flight per wave, profiles/r05/edge_pf/.)
-template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB, int LSP>
+template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB, int LSP, int BS>
 __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, const YView &Y, double *__restrict__ dy,
                                          int i, int cur, const DevDiag &dg, const DevLake &lk, const double *lct,
                                          const OwnRec &own) {
@@ -408,7 +423,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     }
 
     const int sfl = own.sfl;
-    const int sfirst = sfl & 0x7fffffff;
+    const int sfirst = sfl & 0x03ffffff;               // bits 26-29: edge sharing (SH), 31: LAI
     const bool lai_on = sfl < 0;                       // bit 31: t_lai > ZERO (set with the step inputs)
     const int iss = cf_iss(cf), nseg = cf_nseg(cf);
     const double infD = CL(infD), ThR = CL(ThetaR);
@@ -536,29 +551,35 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     }
     if (i >= nown) return;    // ghost element of a partition: vertical + segments only
 
-    // ---- fun_Ele_surface / fun_Ele_sub, one edge per (rolled) iteration (MD_ElementFlux.cpp:35-156) ----
-    // each edge's neighbour data is loaded at the top of its iteration; keeping the loop rolled holds the
-    // kernel at <= 96 VGPRs = 5 waves/SIMD (all three edges in flight at once needs ~145 = 3 waves: slower)
-    double sumsurf = qe2r_surf, sumsub = qe2r_sub;     // QeleSurfTot = Qe2r + sum_j QeleSurf[j]
+    // ---- fun_Ele_surface / fun_Ele_sub (MD_ElementFlux.cpp:35-156) ----
+    // edge(j): edge j's QeleSurf (qsf) and QeleSub before fu_Sub (q).  Its neighbour data is loaded at the top of
+    // each evaluation and the callers keep their loops rolled (<= 96 VGPRs = 5 waves/SIMD; all three edges in flight
+    // at once needs ~145 = 3 waves: slower).  sh (interior edges, SH below): bit 0 the neighbour's QeleSurf for this
+    // edge is -qsf (else qsf), bit 1 its QeleSub before fu_Sub is -q (else q), bit 2 neither head difference is NaN.
     bool nan_q = false;
     const double isf = usf < 0. ? 0. : usf;
     const double area = ldnt(at(p.area, o8));          // in flight across the edge loop
     const int n_edges = is_lake ? 0 : 3;               // lake elements: fun_Ele_lakeHorizon, all zero
-#pragma unroll 1
-    for (int j = 0; j < n_edges; j++) {
+    constexpr bool SH = kShareOn(LCT, GH, LAKE, HYB, DIAG) && BS == kEleBS;   // in-tile edge sharing, below
+    auto edge = [&](int j, double &qsf, double &q, uint32_t &sh) __attribute__((always_inline)) {
         const int nb = j == 0 ? mt.x : j == 1 ? mt.y : mt.z;
         const int nc = nb >= 0 ? nb : i;                  // boundary edge: harmless in-bounds loads
         // (edge 0's loads issued right after the own record instead — held through the vertical physics — took
         // the kernel to 96 VGPRs with spills and measured 0.707 vs 0.617 ms, profiles/r03/ab_prologue/)
         const uint32_t n16 = (uint32_t)nc << 4, n8 = (uint32_t)nc << 3;
-        const double2 g = ldnt2(at(p.ged + (size_t)j * NEl, o16));
+        // (a 32-bit byte offset: j is per lane under SH, and a 64-bit pointer per lane cost a spilled VGPR and +3 %)
+        const double2 g = ldnt2(at(p.ged, o16 + (uint32_t)j * ((uint32_t)NEl << 4)));
         const double2 nzz = *at(p.zz, n16);
         const int ncf = *at((const int *)p.meta + 3, n16);
         const double nsf_raw = GH ? Y.sf(nc) : *at(Y.y, n8);
         const double ngw_raw = GH ? Y.gw(nc) : *at(Y.y + 2 * (size_t)nown, n8);
         const double B = g.x, d2n = g.y;
         const Recip R2 = recip_nr(d2n);                   // both Dist2Nabor divisions of the edge share 1/d2n
-        double qsf = 0., qsb = 0.;
+        qsf = 0.; q = 0.; sh = 0u;
+        // (SH: the own depression and roughness re-read from the LDS class table per edge instead of held in four
+        // VGPRs across the edge section)
+        const double dep_e = SH ? (double)((lds_vd *)lct)[cid * CF_LDS_STRIDE + CfPos<CF_depression>::v] : dep;
+        const double rgh_e = SH ? (double)((lds_vd *)lct)[cid * CF_LDS_STRIDE + CfPos<CF_rough>::v] : rgh;
         const int cn = cf_class(ncf);
 #define CN(f) (LCT ? lct[cn * CF_LDS_STRIDE + CfPos<CF_##f>::v] : p.ctab[cn * CF_STRIDE + CfPos<CF_##f>::v])
         double hvn[4] = {0., 0., 0., 0.};                 // HYB: the neighbour's streamed fields (if it reads any)
@@ -572,7 +593,6 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
             const double nsf = yl < 0. ? 0. : yl;
             qsf = weir_jtoi(zl, nsf, zs, isf, zs, 0.6, B, 0.01);          // MD_ElementFlux.cpp:46-53
             const double dhg = (ugw + zb) - (yl + zl);                   // MD_ElementFlux.cpp:107-121
-            double q = 0.;
             if (dhg > 0. && ugw <= 0.02) q = 0.;
             else if (dhg < 0. && yl <= 0.02) q = 0.;
             else {
@@ -583,25 +603,27 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
             }
             lk.bank_qs[(size_t)j * NEl + i] = qsf;
             lk.bank_qg[(size_t)j * NEl + i] = q;
-            qsb = q * fu_sub;
         } else if (nb >= 0) {
             double nsf = nsf_raw;
             if (MODE == 1) nsf = (nsf >= 0.) ? nsf : 0.;
             nsf = nsf < 0. ? 0. : nsf;
             const double zsn = nzz.x;
             const double dh = (isf + zs) - (nsf + zsn);
-            double ym = ((isf + zs) > (nsf + zsn)) ? ((isf > dep) ? isf : 0.) : ((nsf > dep) ? nsf : 0.);
+            [[maybe_unused]] const bool dh_nz = dh != 0., dh_ok = dh == dh;
+            double ym = ((isf + zs) > (nsf + zsn)) ? ((isf > dep_e) ? isf : 0.) : ((nsf > dep_e) ? nsf : 0.);
             ym = rmin(ym, K_MAXYSURF);
+            bool mu = false;                              // Manning evaluated
             if (ym > 0.) {
                 const double s = div_nr(dh, R2);
                 if (s > 0 && isf <= 0) qsf = 0.;
                 else if (s < 0 && nsf <= 0) qsf = 0.;
-                else qsf = manning(ym * B, 0.5 * (rgh + CNH(rough)), ym, s);  // avgRough, Element.cpp:253
+                else { qsf = manning(ym * B, 0.5 * (rgh_e + CNH(rough)), ym, s); mu = true; }  // avgRough, Element.cpp:253
             }
             const double ugn = ugw_pk<MODE>(m, ngw_raw, cf_ibc(ncf), nb);
             const double zbn = nzz.y;
             const double dhg = (ugw + zb) - (ugn + zbn);
-            double q = 0.;
+            [[maybe_unused]] const bool dhg_nz = dhg != 0., dhg_ok = dhg == dhg;
+            bool zq = true;                               // one of the two zero branches
             if (dhg > 0. && ugw <= 0.02) q = 0.;
             else if (dhg < 0. && ugn <= 0.02) q = 0.;
             else {
@@ -610,29 +632,107 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
                 const double grad = div_nr(dhg, R2);
                 const double kmean = 0.5 * (ekh + ekn);
                 q = kmean * grad * ymg * B;
+                zq = false;
             }
-            qsb = q * fu_sub;
-        } else if (!OPEN) {
-            qsb = 0. * fu_sub;                            // closed boundary: Q = 0, times fu_Sub
-        } else {
+            if constexpr (SH) sh = (mu && dh_nz ? 1u : 0u) | (!zq && dhg_nz ? 2u : 0u) | (dh_ok && dhg_ok ? 4u : 0u);
+        } else if (OPEN) {
             const double d2e = m.dist2edge[j * NEl + i];
-            if (isf > dep) {
+            if (isf > dep_e) {
                 const double s = isf / d2e * 0.5;
-                if (s > 0.) qsf = sqrt(s) * cbrt(isf * isf * isf * isf * isf) * B / rgh;
+                if (s > 0.) qsf = sqrt(s) * cbrt(isf * isf * isf * isf * isf) * B / rgh_e;
             }
-            double q = 0.;
-            if (ugw > dep * 10.) {
+            if (ugw > dep_e * 10.) {
                 const double grad = ugw / d2e * 0.5;
                 if (grad > 0.) q = ekh * grad;
             }
-            qsb = q * fu_sub;
-        }
+        }                                                 // closed boundary: Q = 0, times fu_Sub
 #undef CN
 #undef CNH
+    };
+    double sumsurf = qe2r_surf, sumsub = qe2r_sub;     // QeleSurfTot = Qe2r + sum_j QeleSurf[j]
+    auto add = [&](int j, double qsf, double q) __attribute__((always_inline)) {
+        const double qsb = q * fu_sub;
         if (MODE == 0) nan_q |= nan_or_inf(qsf) || nan_or_inf(qsb);
         sumsurf += qsf;
         sumsub += qsb;
         if (DIAG) { dg.qele_surf[j * NEl + i] = qsf; dg.qele_sub[j * NEl + i] = qsb; }
+    };
+    // SH: in-tile edge sharing.  The host marks (seg_first bits 26-29) interior edges between two elements of one
+    // 256-element tile whose fluxes are exactly antisymmetric — the same edge length and Dist2Nabor bits on both sides,
+    // the same depression, a positive avgRough, no lake — and orients them so that every element publishes at most one
+    // edge and receives at most one.  From both sides the edge evaluates the same operands with dh, dhg (and the
+    // Manning slope) negated exactly, the same ym, kmean, ymg and zero-branch choices, so the neighbour's values are
+    // the publisher's negated — except where the negation would turn a +0 into -0: no Manning / a zero branch (both
+    // sides +0), dh == +0 or dhg == +0 (both sides compute the same +-0 operands).  The publisher evaluates its edge
+    // first and leaves the receiver's values in the LDS slot of its thread (the pow tables' region, dead once every
+    // wave is past satKfun), keeping the two sign bits to recover its own; the receiver takes them after a barrier, or
+    // evaluates the edge itself when the slot holds kShareVoid (a NaN head difference).  The remaining edges are then
+    // evaluated one per iteration with a per-lane slot (a paired element: one), so a wave of paired elements makes two
+    // edge evaluations instead of three, and the sums keep the reference's slot order.  syn-10M: 99.6 % of the
+    // elements receive an edge; element kernel -2.0 %, wall per eval -3.4 % (profiles/r06/share/).
+    if constexpr (!SH) {
+#pragma unroll 1
+        for (int j = 0; j < n_edges; j++) {
+            double qsf, q;
+            uint32_t sh;
+            edge(j, qsf, q, sh);
+            add(j, qsf, q);
+        }
+    } else {
+        // xq[t], xq[kEleBS + t]: the receiver's {QeleSurf, QeleSub before fu_Sub} of thread t's published edge, or
+        // kShareVoid in the first when a head difference was NaN (the receiver then evaluates the edge itself)
+        lds_vd *xq = (lds_vd *)(lct + p.pt_off);
+        const int tid = (int)threadIdx.x;
+        // st: bits 0-1 the published slot + 1, 2-3 the received slot + 1, 4-5 the published edge's sh (own values =
+        // the LDS values with these signs undone), 8-10 the slots still to be taken from LDS — one register for all of
+        // it: the loop below runs at the kernel's VGPR peak
+        uint32_t st = ((uint32_t)sfl >> 26) & 15u;
+        __syncthreads();                                  // every wave is past satKfun's pow-table reads
+        if (st & 3u) {
+            double qsf, q;
+            uint32_t sh;
+            edge((int)(st & 3u) - 1, qsf, q, sh);
+            xq[tid] = (sh & 4u) ? ((sh & 1u) ? -qsf : qsf) : __builtin_bit_cast(double, kShareVoid);
+            xq[kEleBS + tid] = (sh & 2u) ? -q : q;
+            st |= (sh & 3u) << 4 | ((sh & 4u) ? 1u << (8 + (st & 3u) - 1) : 0u);   // void: evaluated again below
+        }
+        __syncthreads();                                  // the published edges are in LDS
+        auto rthread = [&]() __attribute__((always_inline)) {   // the publisher of the received edge
+            const int jr = (int)((st >> 2) & 3u) - 1;
+            return (jr == 0 ? mt.x : jr == 1 ? mt.y : mt.z) - (i - tid);
+        };
+        if (st & 12u) {
+            const int rt = rthread();
+            if (rt >= 0 && rt < kEleBS && __builtin_bit_cast(uint64_t, (double)xq[rt]) != kShareVoid)
+                st |= 1u << (8 + ((st >> 2) & 3u) - 1);
+        }
+        auto take = [&](int mm) __attribute__((always_inline)) {
+            double qsf, q;
+            if (mm == (int)(st & 3u) - 1) {               // own published edge: undo the receiver's signs
+                const double a = xq[tid], b = xq[kEleBS + tid];
+                qsf = (st & 16u) ? -a : a;
+                q = (st & 32u) ? -b : b;
+            } else {
+                const int rt = rthread();
+                qsf = xq[rt];
+                q = xq[kEleBS + rt];
+            }
+            add(mm, qsf, q);
+        };
+#pragma unroll 1
+        for (uint32_t om = 7u & ~(st >> 8); om; om &= om - 1) {
+            const int j = __builtin_ctz(om);
+            double qsf, q;
+            uint32_t sh;
+            edge(j, qsf, q, sh);
+#pragma unroll
+            for (int mm = 0; mm < 2; mm++)
+                if ((st >> (8 + mm) & 1u) && mm < j) { take(mm); st &= ~(1u << (8 + mm)); }
+            add(j, qsf, q);
+        }
+#pragma unroll
+        for (int mm = 0; mm < 3; mm++)
+            if (st >> (8 + mm) & 1u) take(mm);
     }
     if (DIAG && is_lake)
         for (int j = 0; j < 3; j++) { dg.qele_surf[j * NEl + i] = 0.; dg.qele_sub[j * NEl + i] = 0.; }

@@ -55,6 +55,7 @@ struct shud_rhs {
     bool packed = false;                 // class-table / 16-byte-record layout in use (DevPacked)
     DevPacked dp{};
     int n_classes = 0;
+    int n_shared = 0;       // interior edges evaluated once (in-tile edge sharing, build_packed)
     bool fu_unit[2] = {true, true};      // fu_Surf / fu_Sub are all 1.0 (cryosphere off): not read
     bool qd_now = false;                 // this eval's element launch wrote DevPacked::qdown (river kernel reads it)
 

@@ -605,6 +605,39 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
             ged[(size_t)j * NE + i] = make_double2(m->edge[(size_t)j * NE + i], m->dist2nabor[(size_t)j * NE + i]);
         sfirst[i] = seg_off[i];
     }
+    // In-tile edge sharing (shud_ele_packed.hip, SH): an interior edge between two elements of one 256-element tile
+    // whose fluxes are exactly antisymmetric (same edge length and Dist2Nabor bits from both sides, same depression,
+    // positive finite avgRough, neither a lake element) is evaluated by one of them and read by the other from LDS.
+    // Greedy in element order: every element publishes at most one edge and receives at most one, never both
+    // directions of one edge.  seg_first bits 26-27: the published slot + 1, bits 28-29: the received slot + 1.
+    // Elements [0, lim): a single-GPU handle's all, a partitioned handle's interior prefix (its ghost-free launch
+    // tiles from element 0; the boundary launch ignores the bits), no hybrid layout; the instantiations without
+    // sharing (diagnostics, lakes, hybrid, the 1024-thread table) ignore them.
+    const int lim = h->n_int > 0 ? h->n_int : (h->n_own == NE ? NE : 0);
+    if (lim > 1 && !hmask && m->num_seg < (1 << 26) && env_knob("SHUD_RHS_SHARE", 1, 0, 1)) {
+        std::vector<signed char> pub(NE, -1), rcv(NE, -1);
+        auto lake_of = [&](int e) { return m->ilake && m->ilake[e] > 0 && h->lakeon; };
+        for (int i = 0; i < lim; i++) {
+            for (int k = 0; k < 3 && rcv[i] < 0; k++) {
+                const int v = m->nabr[(size_t)k * NE + i];
+                if (v < 0 || v >= lim || v == i || (v / kShareTile) != (i / kShareTile) || pub[v] >= 0) continue;
+                int kk = -1, hits = 0;
+                for (int q = 0; q < 3; q++)
+                    if (m->nabr[(size_t)q * NE + v] == i) { kk = q; hits++; }
+                if (hits != 1 || pub[i] == k) continue;
+                const size_t a = (size_t)k * NE + i, b = (size_t)kk * NE + v;
+                const double ar = m->avg_rough[a];
+                if (memcmp(&m->edge[a], &m->edge[b], 8) || memcmp(&m->dist2nabor[a], &m->dist2nabor[b], 8) ||
+                    memcmp(&m->depression[i], &m->depression[v], 8) || memcmp(&ar, &m->avg_rough[b], 8) ||
+                    !(ar > 0. && std::isfinite(ar)) || lake_of(i) || lake_of(v))
+                    continue;
+                pub[v] = (signed char)kk;
+                rcv[i] = (signed char)k;
+            }
+        }
+        for (int i = 0; i < NE; i++) sfirst[i] |= ((pub[i] + 1) << 26) | ((rcv[i] + 1) << 28);
+        h->n_shared = (int)std::count_if(rcv.begin(), rcv.end(), [](signed char r) { return r >= 0; });
+    }
     int rc;
     DevPacked &P = h->dp;
     double *ctab_d, *area_d; double2 *zz_d, *ged_d; int4 *meta_d; int *sf_d;
@@ -1118,6 +1151,12 @@ extern "C" long long shud_rhs_num_calls(shud_rhs_t h) { return h ? h->ncalls : -
 extern "C" int shud_rhs_layout_streamed(shud_rhs_t h, int *n_streamed) {
     if (!h || !n_streamed) return shud_fail(SHUD_ERR_ARG, "null argument");
     *n_streamed = h->packed ? h->dp.nh : 0;
+    return SHUD_OK;
+}
+
+extern "C" int shud_rhs_layout_shared(shud_rhs_t h, int *n_shared) {
+    if (!h || !n_shared) return shud_fail(SHUD_ERR_ARG, "null argument");
+    *n_shared = h->packed ? h->n_shared : 0;
     return SHUD_OK;
 }
 

@@ -169,6 +169,7 @@ FUNCTIONS = {
     "shud_rhs_num_calls": (C.c_longlong, [_H]),
     "shud_rhs_layout": (C.c_int, [_H, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "shud_rhs_layout_streamed": (C.c_int, [_H, C.POINTER(C.c_int)]),
+    "shud_rhs_layout_shared": (C.c_int, [_H, C.POINTER(C.c_int)]),
     "shud_rhs_destroy": (C.c_int, [_H]),
     "shud_rhs_last_error_string": (C.c_char_p, []),
     "shud_rhs_cvrhs": (C.c_int, [C.c_double, C.c_void_p, C.c_void_p, C.c_void_p]),
@@ -243,9 +244,12 @@ OUT_FUNCTIONS = {
 }
 
 
-def bind(lib):
+def bind(lib, strict=True):
+    """set the signatures; strict=False (A/B builds of older sources) skips symbols the library lacks"""
     for name, (res, args) in (list(FUNCTIONS.items()) + list(ET_FUNCTIONS.items()) + list(ODE_FUNCTIONS.items())
                               + list(OUT_FUNCTIONS.items())):
+        if not strict and not hasattr(lib, name):
+            continue
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args

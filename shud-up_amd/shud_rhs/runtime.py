@@ -117,9 +117,14 @@ class RhsHandle:
         pk, nc, ns = C.c_int(), C.c_int(), C.c_int()
         _check(lib().shud_rhs_layout(self.h, C.byref(pk), C.byref(nc)), "shud_rhs_layout")
         _check(lib().shud_rhs_layout_streamed(self.h, C.byref(ns)), "shud_rhs_layout_streamed")
+        sh = C.c_int()
+        if hasattr(lib(), "shud_rhs_layout_shared"):     # (A/B builds of older sources lack it)
+            _check(lib().shud_rhs_layout_shared(self.h, C.byref(sh)), "shud_rhs_layout_shared")
         out = {"packed": bool(pk.value), "n_classes": nc.value}
         if ns.value:
             out["streamed_fields"] = ns.value
+        if sh.value:
+            out["shared_edges"] = sh.value
         return out
 
     def diagnostics(self):

@@ -44,7 +44,7 @@ def lib_for(v):
         return runtime.lib() if "prod" not in _libs else _libs["prod"]
     name = v[4:].split("+", 1)[0]
     if name not in _libs:
-        _libs[name] = abi.bind(C.CDLL(os.path.join(ROOT, "shud-up_amd", "build", "ab", f"libshud_rhs_{name}.so")))
+        _libs[name] = abi.bind(C.CDLL(os.path.join(ROOT, "shud-up_amd", "build", "ab", f"libshud_rhs_{name}.so")), strict=False)
     return _libs[name]
 
 
