@@ -9,6 +9,6 @@ if [ "${SUITE:-0}" = 1 ]; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
 fi
 for n in "$@"; do
-  timeout -k 10 ${ABT:-400} python tools/ab_variants.py --n-ele $n --variants $V --rounds $R --reps 50 > $O/abv_$n.log 2>&1
+  timeout -k 10 ${ABT:-400} python tools/ab_variants.py --n-ele $n --variants $V --rounds $R --reps 50 ${ABX:-} > $O/abv_$n${ABS:-}.log 2>&1
 done
 echo done

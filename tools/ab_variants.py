@@ -24,12 +24,16 @@ ap.add_argument("--variants", default="soa,pk",
                      "pk+NAME=VAL = pk with run-time switches; lib:NAME = an A/B library build")
 ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--reps", type=int, default=20)
+ap.add_argument("--ksath-mod", type=int, default=0,
+                help="KsatH * (1 + 1e-7 (i %% K)): about 33 K parameter classes (K = 2: the 36..128-class LDS table)")
 ap.add_argument("--many-class", action="store_true",
                 help="KsatH per element (bench.py many_class: 13,200 tuples -> the hybrid layout)")
 a = ap.parse_args()
 m = synth.synth_model(a.n_ele)
 m.step = workload.random_step_inputs(m)
 y = workload.random_state(m)
+if a.ksath_mod > 1:
+    m.par["KsatH"] = m.par["KsatH"] * (1.0 + 1e-7 * (np.arange(m.num_ele) % a.ksath_mod))
 if a.many_class:
     m.par["KsatH"] = m.par["KsatH"] * (1.0 + 1e-7 * (np.arange(m.num_ele) % 400))
 vs = a.variants.split(",")
