@@ -36,6 +36,9 @@ def _run_ranks(m, y_list, locs, mode, ncalls=3, device_eval=False):
             ny = 3 * part.n_own_ele + part.n_own_riv + part.n_own_lake
             bufs.append((h.device_alloc(8 * ny), h.device_alloc(8 * ny), ny))
             halos.append(h.halo_buffers())
+        # in-tile edge sharing (shud_rhs.cpp build_packed) covers a rank's interior prefix as well
+        if single.layout().get("shared_edges"):
+            assert sum(h.layout().get("shared_edges", 0) for h in hs) > 0, [h.layout() for h in hs]
         for yy in y_list:
             for call in range(ncalls):
                 ref = single.eval(0.0, yy)
