@@ -426,6 +426,9 @@ def main():
             "frac": achieved / HBM_PEAK,
             "traffic": None,
             "algorithmic_bytes_per_launch": ele_bytes,
+            "frac_note": ("achieved / frac price SURVEY §8d's canonical 392 B per element, which counts every edge's "
+                          "neighbour gathers as HBM reads (L2 hits in practice; shared in-tile edges gather nothing), "
+                          "so frac can exceed 1; traffic / frac_actual are the PMC-measured bytes"),
             "kernel_ms": {k: v for k, v in per.items()},
             "kernel_ms_source": (f"HIP events around the kernels of {n_timed} of the {args.steps} timed evals "
                                  f"(1 in {t_stride}; handle stream)"),
