@@ -96,6 +96,11 @@ constexpr int kLdsClassMax = 128;
 // elements per workgroup of the packed element kernel (shud_ele_packed.hip kEleBS): the tiles the host's edge-sharing
 // assignment (shud_rhs.cpp, seg_first bits 26-29) pairs elements within
 constexpr int kShareTile = 256;
+// the parked DY tail of the packed element kernel (shud_ele_packed.hip LSP): kLspN doubles + one int per thread
+// beside the ntab-double class + pow tables, taken while a workgroup's LDS stays <= kLspLdsMax (7 per CU)
+constexpr int kLspN = 5;
+constexpr size_t kLspLdsMax = 23296;
+constexpr size_t lsp_lds_bytes(int ntab) { return (size_t)(ntab + kLspN * kShareTile) * 8 + kShareTile * 4; }
 // pow_tab's log + exp tables (shud_pow_tab.h: 256 x 4 + 128 x 2 doubles; SHUD_PT_COMPACT: 128 x 2.5 + 128 x 2), staged in
 // LDS after the class table (shud_rhs.cpp checks the sizes against the generated tables)
 #ifndef SHUD_PT_COMPACT

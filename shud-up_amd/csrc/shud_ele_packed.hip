@@ -93,9 +93,11 @@ constexpr bool kShareOn(bool lct, bool gh, bool lake, int hyb, bool diag) {
     return lct && !gh && !lake && hyb == 0 && !diag;
 }
 // min waves per SIMD of an instantiation: with sharing and the parked DY tail 7 (72 VGPRs, no spills with FU1; 6
-// without FU1, where 7 would spill), others 5
-constexpr int kEleWavesOf(bool lct, int lspk, bool gh, bool lake, int hyb, bool diag, bool fu1) {
-    return (kShareOn(lct, gh, lake, hyb, diag) && lspk) ? (fu1 ? kEleWavesSh : 6) : kEleWaves;
+// without FU1, where 7 would spill); the plain LDS-table one (36..~128 classes) 6 on closed boundaries (80 VGPRs, no
+// spills; its unbounded allocation drifts between 80 and 86 with unrelated code), others 5
+constexpr int kEleWavesOf(bool lct, int lspk, bool gh, bool lake, int hyb, bool diag, bool fu1, bool open) {
+    return (kShareOn(lct, gh, lake, hyb, diag) && lspk) ? (fu1 ? kEleWavesSh : 6)
+           : (kShareOn(lct, gh, lake, hyb, diag) && !open) ? 6 : kEleWaves;
 }
 constexpr int kEleBS = 256;       // elements per workgroup
 static_assert(kEleBS == kShareTile, "edge sharing pairs elements within one workgroup's tile");
@@ -207,14 +209,13 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
 // 11 KiB of LDS per workgroup, so the handle takes this instantiation only while 7 workgroups still fit in a CU's
 // 160 KiB (kLspLdsMax: 23,296 B per workgroup, the runtime's occupancy answer on gfx950, tools/lds_occ.hip), i.e. up
 // to ~35 parameter classes, and never for the diagnostic, lake or hybrid instantiations.
-constexpr int kLspN = 5;
-constexpr size_t kLspLdsMax = 23296;
+// (kLspN, kLspLdsMax, lsp_lds_bytes: shud_dev.h, shared with the host's edge-sharing assignment)
 
 // HYB: the hybrid layout (DevPacked::hv): the streamed class fields come from the element's (and its neighbours')
 // per-element record, the rest from the LDS class table; 1 = one streamed field (one 8-B value per element, held in
 // one register pair), 2 = two to four
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB = 0, int LSPK = 0>
-__global__ void __launch_bounds__(kEleBS, kEleWavesOf(LCT, LSPK, GH, LAKE, HYB, DIAG, FU1))
+__global__ void __launch_bounds__(kEleBS, kEleWavesOf(LCT, LSPK, GH, LAKE, HYB, DIAG, FU1, OPEN))
 shud_ele_kernel_packed(DevMesh m, DevPacked p, YView Y, double *__restrict__ dy, int i0, int n_compute, int cur,
                        DevDiag dg, DevLake lk, int per8, int nb_q, int q0) {
     extern __shared__ double lct[];                       // ntab doubles (class table + pow tables) when LCT
@@ -423,7 +424,11 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     }
 
     const int sfl = own.sfl;
-    const int sfirst = sfl & 0x03ffffff;               // bits 26-29: edge sharing (SH), 31: LAI
+    // bits 26-29: edge sharing (SH), 31: LAI.  The host assigns sharing bits only to handles that take the LSP
+    // instantiations (lsp_lds_bytes), without lakes or the hybrid layout, so the plain LDS-table, big-table, lake and
+    // hybrid instantiations never see them and keep the 31-bit mask (the 26-bit one costs the plain LDS-table
+    // kernel 6 VGPRs: 80 -> 86, 6 -> 5 waves)
+    const int sfirst = sfl & ((LSP || DIAG || !LCT) ? 0x03ffffff : 0x7fffffff);
     const bool lai_on = sfl < 0;                       // bit 31: t_lai > ZERO (set with the step inputs)
     const int iss = cf_iss(cf), nseg = cf_nseg(cf);
     const double infD = CL(infD), ThR = CL(ThetaR);
@@ -560,7 +565,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     const double isf = usf < 0. ? 0. : usf;
     const double area = ldnt(at(p.area, o8));          // in flight across the edge loop
     const int n_edges = is_lake ? 0 : 3;               // lake elements: fun_Ele_lakeHorizon, all zero
-    constexpr bool SH = kShareOn(LCT, GH, LAKE, HYB, DIAG) && BS == kEleBS;   // in-tile edge sharing, below
+    constexpr bool SH = kShareOn(LCT, GH, LAKE, HYB, DIAG) && LSP != 0 && BS == kEleBS;   // edge sharing, below
     auto edge = [&](int j, double &qsf, double &q, uint32_t &sh) __attribute__((always_inline)) {
         const int nb = j == 0 ? mt.x : j == 1 ? mt.y : mt.z;
         const int nc = nb >= 0 ? nb : i;                  // boundary edge: harmless in-bounds loads
@@ -1090,7 +1095,7 @@ static int qd_start(int nb, int pm) {
 // dynamic LDS of the 256-thread packed kernel: the class + pow tables, and with LSPK the parked DY-tail slots
 static size_t lds_bytes(const DevPacked &p, bool lct, bool lspk) {
     if (!lct) return 0;
-    return (size_t)(p.ntab + (lspk ? kLspN * kEleBS : 0)) * sizeof(double) + (lspk ? kEleBS * sizeof(int) : 0);
+    return lspk ? lsp_lds_bytes(p.ntab) : (size_t)p.ntab * sizeof(double);
 }
 template <int MODE, bool OPEN, bool DIAG, bool FU1, bool LCT, bool LAKE, bool GH, int HYB = 0, int LSPK = 0>
 static void launch_p(const DevMesh &m, const DevPacked &p, const YView &Y, double *dy, int i0, int i1, int cur,

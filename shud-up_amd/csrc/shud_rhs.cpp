@@ -614,7 +614,10 @@ static int build_packed(shud_rhs *h, const ShudMeshSoA *m, const ShudParamsSoA *
     // tiles from element 0; the boundary launch ignores the bits), no hybrid layout; the instantiations without
     // sharing (diagnostics, lakes, hybrid, the 1024-thread table) ignore them.
     const int lim = h->n_int > 0 ? h->n_int : (h->n_own == NE ? NE : 0);
-    if (lim > 1 && !hmask && m->num_seg < (1 << 26) && env_knob("SHUD_RHS_SHARE", 1, 0, 1)) {
+    // Only for handles that take the LSP instantiations (class + pow tables small enough, no lakes, no hybrid
+    // layout): the other instantiations read seg_first with a 31-bit mask (shud_ele_packed.hip ele_body).
+    if (lim > 1 && !hmask && !h->lakeon && lsp_lds_bytes((int)ctab.size()) <= kLspLdsMax && m->num_seg < (1 << 26) &&
+        env_knob("SHUD_RHS_SHARE", 1, 0, 1)) {
         std::vector<signed char> pub(NE, -1), rcv(NE, -1);
         auto lake_of = [&](int e) { return m->ilake && m->ilake[e] > 0 && h->lakeon; };
         for (int i = 0; i < lim; i++) {
