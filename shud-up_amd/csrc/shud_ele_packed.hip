@@ -671,10 +671,11 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
     // sides +0), dh == +0 or dhg == +0 (both sides compute the same +-0 operands).  The publisher evaluates its edge
     // first and leaves the receiver's values in the LDS slot of its thread (the pow tables' region, dead once every
     // wave is past satKfun), keeping the two sign bits to recover its own; the receiver takes them after a barrier, or
-    // evaluates the edge itself when the slot holds kShareVoid (a NaN head difference).  The remaining edges are then
-    // evaluated one per iteration with a per-lane slot (a paired element: one), so a wave of paired elements makes two
-    // edge evaluations instead of three, and the sums keep the reference's slot order.  syn-10M: 99.6 % of the
-    // elements receive an edge; element kernel -2.0 %, wall per eval -3.4 % (profiles/r06/share/).
+    // evaluates the edge itself when the slot holds kShareVoid (a NaN head difference).  A lane without a publication
+    // evaluates one of its own edges in that first pass instead.  The remaining edges are then evaluated one per
+    // iteration with a per-lane slot (a paired element: one), so a wave makes two edge-evaluation passes instead of
+    // three unless it holds the one element per tile path that must evaluate three; the sums keep the reference's
+    // slot order.  syn-10M: 99.6 % of the elements receive an edge (profiles/r06/share/).
     if constexpr (!SH) {
 #pragma unroll 1
         for (int j = 0; j < n_edges; j++) {
@@ -688,18 +689,25 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
         // kShareVoid in the first when a head difference was NaN (the receiver then evaluates the edge itself)
         lds_vd *xq = (lds_vd *)(lct + p.pt_off);
         const int tid = (int)threadIdx.x;
-        // st: bits 0-1 the published slot + 1, 2-3 the received slot + 1, 4-5 the published edge's sh (own values =
-        // the LDS values with these signs undone), 8-10 the slots still to be taken from LDS — one register for all of
-        // it: the loop below runs at the kernel's VGPR peak
+        // st: bits 0-1 the published slot + 1, 2-3 the received slot + 1, 4-5 the sh signs of the thread's own LDS
+        // slot (own values = the LDS values with these signs undone), 8-10 the slots still to be taken from LDS, 12-13
+        // the first pass's slot + 1 — one register for all of it: the loop below runs at the kernel's VGPR peak
         uint32_t st = ((uint32_t)sfl >> 26) & 15u;
+        // first pass, every lane: its published edge, or else its lowest slot that is not the received one, whose
+        // values then wait in the thread's own (unpublished) LDS slot — so an element that only receives (a tile's
+        // first) makes its two evaluations in the two passes the wave makes anyway
+        const int jr0 = (int)((st >> 2) & 3u) - 1;
+        const int j1 = (st & 3u) ? (int)(st & 3u) - 1 : (jr0 == 0 ? 1 : 0);
+        st |= (uint32_t)(j1 + 1) << 12;
         __syncthreads();                                  // every wave is past satKfun's pow-table reads
-        if (st & 3u) {
+        {
             double qsf, q;
             uint32_t sh;
-            edge((int)(st & 3u) - 1, qsf, q, sh);
+            edge(j1, qsf, q, sh);
+            if (!(st & 3u)) sh = 4u;                      // not a publication: raw values, always taken back
             xq[tid] = (sh & 4u) ? ((sh & 1u) ? -qsf : qsf) : __builtin_bit_cast(double, kShareVoid);
             xq[kEleBS + tid] = (sh & 2u) ? -q : q;
-            st |= (sh & 3u) << 4 | ((sh & 4u) ? 1u << (8 + (st & 3u) - 1) : 0u);   // void: evaluated again below
+            st |= (sh & 3u) << 4 | ((sh & 4u) ? 1u << (8 + j1) : 0u);   // void: evaluated again below
         }
         __syncthreads();                                  // the published edges are in LDS
         auto rthread = [&]() __attribute__((always_inline)) {   // the publisher of the received edge
@@ -713,7 +721,7 @@ __device__ __forceinline__ void ele_body(const DevMesh &m, const DevPacked &p, c
         }
         auto take = [&](int mm) __attribute__((always_inline)) {
             double qsf, q;
-            if (mm == (int)(st & 3u) - 1) {               // own published edge: undo the receiver's signs
+            if (mm == (int)((st >> 12) & 3u) - 1) {       // the thread's own slot: undo the receiver's signs
                 const double a = xq[tid], b = xq[kEleBS + tid];
                 qsf = (st & 16u) ? -a : a;
                 q = (st & 32u) ? -b : b;
