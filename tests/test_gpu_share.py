@@ -124,11 +124,11 @@ def test_share_nonfinite_heads(kind, oracle_mod, monkeypatch):
         y[k[:3] + 1] = np.inf                          # neighbours both infinite: inf - inf = NaN head difference
     ga, ea = _run(a, y)
     gb, eb = _run(b, y)
-    _, code, idx, kind = o.eval(0.0, y)
+    _, code, idx, ekind = o.eval(0.0, y)
     assert ea == eb, (ea, eb)
     if code:
         assert ea is not None and ea["exit_code"] == code
-        if kind == abi.EF_NAN_QELE:                          # CheckNANij: the first element with a NaN lateral flux
+        if ekind == abi.EF_NAN_QELE:                          # CheckNANij: the first element with a NaN lateral flux
             assert ea["first_index"][0] == idx, (ea["first_index"], idx)
     else:
         _same_bits(ga, gb, kind)
