@@ -154,3 +154,30 @@ def test_share_counts_real_meshes(monkeypatch):
         print(name, m.num_ele, a.layout())
         a.close()
         b.close()
+
+
+from hypothesis import HealthCheck, given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+
+@settings(max_examples=10, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+@given(n=st.integers(2000, 30000), seed=st.integers(0, 10_000), mode=st.sampled_from([0, 1]),
+       open_boundary=st.booleans())
+def test_share_random_meshes(n, seed, mode, open_boundary, monkeypatch):
+    """drawn branch-variant meshes (sizes that end in a partial tile, either boundary kind, both modes): sharing on
+    vs off bit for bit, for a random state and the equal-head / dry-cell states"""
+    m, _ = cases.variant(n, seed=seed)
+    m.close_boundary = 0 if open_boundary else 1
+    m.step = workload.random_step_inputs(m, seed=seed + 7)
+    a, b = _handles(m, mode, monkeypatch)
+    try:
+        for si, y in enumerate(_states(m, seed)[:3]):
+            ga, ea = _run(a, y)
+            gb, eb = _run(b, y)
+            assert ea == eb, (ea, eb)
+            if ea is None:
+                _same_bits(ga, gb, f"n={n} seed={seed} state {si}")
+    finally:
+        a.close()
+        b.close()
